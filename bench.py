@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""bench.py -- MCMC proposals/s of the rj-MCMC t* chain on MI355X.
+
+Metric (BASELINE.json): MCMC proposals/sec (likelihood evaluations/sec) at 381
+rays x N cells.  Workload (BASELINE configs[2], the north-star target): the
+381 shipped rays, a 5000-cell starting model (seed 3), one chain per GPU
+running the reference's birth/death/change/move mix
+(TD_inversion_function.jl:72) with the DEVICE engine.  max_cells is raised to
+2N so births stay active (the reference default of 100 would freeze N).
+
+A "step" = --iters-per-step chain iterations (proposals), each one a complete
+forward-model evaluation of the proposed model -- bit-identical to a full
+evaluate (tests/test_gpu_chain.py) -- plus the Metropolis-Hastings decision.
+Inputs are resident in HBM before the timed region.  value = proposals of
+all ranks / max-over-ranks wall time (weak scaling: one chain per GPU,
+independent chains, no data-path collective).
+
+Also reported:
+  roofline      -- k_chain_run (the only kernel in the timed region): the
+                   algorithmic bytes its proposals read (counted in-kernel)
+                   / its HIP-event time, against HBM peak.
+  full_evaluate -- the drop-in td_evaluate path (brute-force P x N nearest
+                   search, MCsub.jl:123-185) on the same model: latency and
+                   the FP64-VALU roofline of its dominant kernel nn_partial.
+  cpu_baseline  -- the CPU oracle (scalar C restatement of evaluate, 1 core)
+                   timed for ~--cpu-seconds: the reference's structure does
+                   one full evaluate per proposal.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
+FP64_VALU_PEAK_TFLOPS = 78.6   # FP64 vector, FMA counted as 2 (spec)
+# the distance kernel may not use FMA (bit-exactness), so its roof is half that
+FP64_NOFMA_PEAK_TFLOPS = FP64_VALU_PEAK_TFLOPS / 2
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cells", type=int, default=5000)
+    ap.add_argument("--iters-per-step", type=int, default=5000)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-full-evaluate", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import tonga
+
+    tt = tonga.load()
+    ds = tt.load_data_Tonga()
+    N = a.cells
+    model = tt.random_model(N, 3)  # config 3: seed 3
+    ctx = tt.TdContext.from_datastruct(ds, device=local)
+    prm = tt.define_TDstructrure().replace(max_cells=2 * N)
+    chain = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000 + rank, chain=1 + rank), model)
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        chain.run(a.iters_per_step)
+    s0 = chain.stats()
+    ctx.timing(enable=True, reset=True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        chain.run(a.iters_per_step)  # synchronous: returns after the kernel finished
+    barrier_sync()
+    el = time.perf_counter() - t0
+    s1 = chain.stats()
+    launches, kms = ctx.timing(kernel="chain_run")
+    ctx.timing(enable=False)
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    iters = a.steps * a.iters_per_step
+    total = iters * world
+    value = total / el
+    P = ctx.P
+    acc = [x - y for x, y in zip(s1["accepted"], s0["accepted"])]
+    prop = [x - y for x, y in zip(s1["proposed"], s0["proposed"])]
+    nbytes = s1["bytes"] - s0["bytes"]
+    bytes_per_launch = nbytes / max(launches, 1)
+    avg_s = kms / 1e3 / max(launches, 1)
+    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    out = {
+        "metric": "MCMC proposals/sec (likelihood evals/sec) at 381 rays x N cells",
+        "value": round(value, 1),
+        "unit": "proposals/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(el / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "381 shipped rays (Data/381raypaths.jld), ak135 slowness substitute, synthetic seeded cells",
+        "config": {"workload": "config3: 381 rays x %d cells, 1 chain/GPU, birth/death/change/move" % N,
+                   "rays": int(ctx.n), "points": P, "cells_start": N, "cells_end": int(s1["ncells"]),
+                   "iters_per_step": a.iters_per_step, "engine": "device", "parallelism": "chains%d" % world},
+        "evals_per_s_equiv": round(value * P * N, 1),
+        "acceptance": {"birth/death/change/move accepted": acc, "proposed": prop,
+                       "rate": round(sum(acc) / max(sum(prop), 1), 4)},
+        "roofline": {"kernel": "k_chain_run", "bound": "hbm", "achieved": round(achieved, 3),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": None, "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
+                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
+                     "note": "one persistent workgroup per chain: latency-bound by design (see DESIGN.md)"},
+    }
+    if rank == 0 and not a.no_full_evaluate:
+        out["full_evaluate"] = full_evaluate(tt, ctx, model, N)
+    if rank == 0 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(ds, model, a.cpu_seconds)
+        if out["cpu_baseline"]["value"] > 0:
+            out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
+    chain.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def full_evaluate(tt, ctx, model, N, reps=50):
+    cells = model.cells()
+    for _ in range(3):
+        ctx.evaluate(cells)
+    ctx.timing(enable=True, reset=True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.evaluate(cells)
+    el = (time.perf_counter() - t0) / reps
+    nl, nn_ms = ctx.timing(kernel="nn_partial")
+    _, mg_ms = ctx.timing(kernel="nn_merge")
+    _, rs_ms = ctx.timing(kernel="ray_sums")
+    _, c2_ms = ctx.timing(kernel="chi2")
+    ctx.timing(enable=False)
+    E = ctx.P * N
+    t_nn = nn_ms / 1e3 / max(nl, 1)
+    flops = 8.0 * E  # 3 sub + 3 mul + 2 add per distance, no FMA allowed
+    tf = flops / t_nn / 1e12
+    return {"evaluate_ms": round(el * 1e3, 4), "evals_per_s": round(E / el, 1),
+            "kernel_ms": {"nn_partial": round(t_nn * 1e3, 4), "nn_merge": round(mg_ms / max(nl, 1), 4),
+                          "ray_sums": round(rs_ms / max(nl, 1), 4), "chi2": round(c2_ms / max(nl, 1), 4)},
+            "roofline": {"kernel": "nn_partial", "bound": "valu-fp64", "achieved": round(tf, 3),
+                         "peak": FP64_NOFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / FP64_NOFMA_PEAK_TFLOPS, 4),
+                         "flops_per_launch": flops}}
+
+
+def cpu_baseline(ds, model, seconds):
+    import oracle  # CPU baseline leg only
+
+    o = oracle.lib()
+    cells = model.cells()
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.evaluate(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig, cells)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    del o
+    return {"value": round(n / el, 3), "unit": "proposals/s", "cores": 1, "kind": "port",
+            "sample": "%d full evaluates (oracle/tstar_oracle.c, scalar FP64, -O2) of the same 381-ray x %d-cell "
+                      "model in %.1f s; the reference evaluates every proposal in full" % (n, len(cells[0]), el)}
+
+
+if __name__ == "__main__":
+    main()

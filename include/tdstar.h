@@ -1,0 +1,190 @@
+/*
+ * tdstar.h -- C ABI of the MI355X-native t* forward model (libtdstar.so).
+ *
+ * Drop-in boundary for the per-proposal hot path of the rj-MCMC Voronoi t*
+ * tomography in Geronimorz/MCMC-in-Tonga (Julia).  Each entry point names the
+ * reference interface it replaces (file:line in the reference tree).  The
+ * signatures use plain pointers and sizes only, so a Julia `ccall`, a Python
+ * `ctypes` binding or a C/C++ host can call them unchanged.
+ *
+ * Conventions
+ *  - All arrays are FP64 unless noted; ray arrays keep the reference's
+ *    DataStruct layout: rayX/rayY/rayZ are m x n COLUMN-MAJOR (ray i = column
+ *    i), tail-padded with NaN; rayL/rayU are (m-1) x n (DefStruct.jl:24-28).
+ *  - Cell indices crossing the ABI are 0-based (Julia adds 1); -1 = "no cell
+ *    closer than the 1e9 sentinel" (MCsub.jl:249-250: v_nearest returns 0.0).
+ *  - Every call returns a td_status; on error the message is available from
+ *    td_last_error(ctx) (td_last_error(NULL) for td_create failures, per
+ *    thread).  No C++ exception crosses the ABI.
+ *  - A context is bound to one device, owns one HIP stream, is NOT thread-
+ *    safe (one context per Julia worker process, main_inversion.jl:15), and
+ *    every call is synchronous: outputs are valid on return.
+ *  - Host buffers are owned by the caller and only read/written during the
+ *    call.  Ray geometry is copied to device memory once, at td_create.
+ */
+#ifndef TDSTAR_H
+#define TDSTAR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TDSTAR_ABI_VERSION 1
+
+typedef struct td_ctx td_ctx;
+typedef struct td_chain td_chain;
+
+typedef enum td_status {
+    TD_OK = 0,
+    TD_ERR_ARG = 1,    /* bad pointer / size / option */
+    TD_ERR_LAYOUT = 2, /* NaN padding of rayX and rayL disagree (Julia: DimensionMismatch) */
+    TD_ERR_HIP = 3,    /* HIP runtime error (message names the call) */
+    TD_ERR_NOMEM = 4,
+    TD_ERR_BOUNDS = 5  /* Y/Z shorter than npoints (Julia: BoundsError) */
+} td_status;
+
+/* ------------------------------------------------------------------------
+ * Context: device-resident copy of DataStruct's hot fields.
+ * Replaces the device half of load_data_Tonga.jl:59-81 (rayX/Y/Z, rayL/U,
+ * tS, allSig).  Validates the NaN layout: for every ray, the number of
+ * leading non-NaN entries of rayL must equal max(npoints-1, 0) where npoints
+ * is the number of leading non-NaN entries of rayX (MCsub.jl:150,312-316).
+ * n may be 0.  device < 0 selects the current HIP device.
+ * ------------------------------------------------------------------------ */
+int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, const double *rayZ,
+              const double *rayL, const double *rayU, int64_t m, int64_t n, const double *tS,
+              const double *allSig);
+int td_destroy(td_ctx *ctx);
+const char *td_last_error(const td_ctx *ctx);
+
+typedef struct td_info {
+    int32_t abi_version;
+    int32_t device;
+    int64_t m, n;         /* DataStruct.rayX size */
+    int64_t npoints;      /* P: valid ray points over all rays */
+    int64_t nsegments;    /* S = P - (rays with >= 1 point) */
+    double likelihood;    /* the MCsub.jl:179 constant for the current allSig */
+    char arch[32];        /* e.g. "gfx950" */
+} td_info;
+int td_get_info(const td_ctx *ctx, td_info *info);
+
+/* Per-kernel device timing with HIP events recorded on the context's stream
+ * around every launch (off by default; used by bench.py for the roofline).
+ * Kernel names: "nn_partial", "nn_merge", "ray_sums", "chi2", "chain_run".
+ * td_timing_get waits for the recorded events and returns the launch count
+ * and summed duration since the last reset. */
+int td_timing_enable(td_ctx *ctx, int enable);
+int td_timing_reset(td_ctx *ctx);
+int td_timing_get(td_ctx *ctx, const char *kernel, int64_t *launches, double *total_ms);
+
+/* Replaces DataStruct.allSig (DefStruct.jl:10) for action 5
+ * (TD_inversion_function.jl:252-261); n values. */
+int td_set_sigma(td_ctx *ctx, const double *allSig);
+
+/* ------------------------------------------------------------------------
+ * evaluate -- replaces MCsub.jl:123-185 `evaluate(model, dataStruct,
+ * TD_parameters)` (interp_style 1, MCsub.jl:326-327).
+ *   cells: Model.xCell/yCell/zCell/zeta (DefStruct.jl:34-37), nCells long,
+ *          in Julia order (tie-breaks follow it).
+ *   debug_prior == 1: phi = likelihood = 1, nothing else written
+ *          (MCsub.jl:134-136).
+ *   ptS_out[n]   -> Model.ptS (MCsub.jl:174)         (nullable)
+ *   phi_out      -> Model.phi (MCsub.jl:169-173)     (nullable)
+ *   likelihood_out -> Model.likelihood (MCsub.jl:179-182) (nullable)
+ *   nearest_out[P] -> 0-based cell chosen for every valid ray point, ray-major
+ *          (what v_nearest computes but never returns)  (nullable)
+ * phi is the sequential chi^2 of MCsub.jl:170-172 and ptS uses Julia's sum
+ * association (oracle/README.md), so both are bit-exact to the CPU oracle.
+ * ------------------------------------------------------------------------ */
+int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const double *zCell,
+                const double *zeta, int64_t nCells, int debug_prior, double *ptS_out, double *phi_out,
+                double *likelihood_out, int32_t *nearest_out);
+
+/* Several models at once (independent chains / tempering replicas on one
+ * GPU): model k's cells are [cell_off[k], cell_off[k+1]) of the cell arrays.
+ * ptS_out is nmodels x n (row k = model k), phi_out/likelihood_out nmodels. */
+int td_evaluate_batch(td_ctx *ctx, int64_t nmodels, const int64_t *cell_off, const double *xCell,
+                      const double *yCell, const double *zCell, const double *zeta, double *ptS_out,
+                      double *phi_out, double *likelihood_out);
+
+/* ------------------------------------------------------------------------
+ * Interpolation -- replaces MCsub.jl:306-336 (interp_style 1), as called for
+ * the birth/death 1-point queries (TD_inversion_function.jl:81,146) and on
+ * grids (MCsub.jl:766-768,800-802).  npoints = leading non-NaN entries of X
+ * (MCsub.jl:312-316); ny == 1 / nz == 1 broadcast (MCsub.jl:317-322);
+ * otherwise ny, nz must be >= npoints (TD_ERR_BOUNDS).  Writes npoints
+ * values to zeta_out (capacity nx) and, if non-NULL, nearest cells to
+ * nearest_out and npoints to *npoints_out.
+ * ------------------------------------------------------------------------ */
+int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const double *zCell,
+                   const double *zeta, int64_t nCells, const double *X, int64_t nx, const double *Y,
+                   int64_t ny, const double *Z, int64_t nz, double *zeta_out, int32_t *nearest_out,
+                   int64_t *npoints_out);
+
+/* ------------------------------------------------------------------------
+ * rj-MCMC chain -- replaces TD_inversion_function.jl:7-305 (one chain) for
+ * prior == 1 (uniform), the default (define_TDstructure.jl:52).  The chain
+ * state (cells, per-point nearest-cell cache, ptS, phi) lives in device
+ * memory; proposals are evaluated incrementally (birth: one new cell vs the
+ * cache; death/move: re-search only the points whose cell changed; change:
+ * no search) and are bit-identical to a full evaluate of the proposed model.
+ * RNG: counter-based Philox4x32-10 keyed by (seed, chain), so runs are
+ * reproducible (the reference seeds from the wall clock, :13).
+ * ------------------------------------------------------------------------ */
+typedef struct td_chain_params {
+    /* define_TDstructure.jl:1-44 fields that reach the chain */
+    int32_t debug_prior;   /* 1: sample the prior (evaluate returns phi = 1) */
+    int32_t sig;           /* percent (10) */
+    int32_t zeta_scale;    /* 50 */
+    int32_t max_cells;     /* 100 */
+    int32_t min_cells;     /* 5 */
+    int32_t prior;         /* only 1 (uniform) is supported: TD_ERR_ARG otherwise */
+    double n_iter, burn_in, keep_each;
+    /* xVec/yVec/zVec extents (DataStruct.xVec etc., min(xVec...), max(xVec...)) */
+    double xmin, xmax, ymin, ymax, zmin, zmax;
+    uint64_t seed;
+    int32_t chain;          /* chain id (TD_inversion_function.jl:10) */
+    double temperature;     /* tempering: acceptance uses phi / temperature (1 = reference) */
+    int32_t engine;         /* TD_ENGINE_DEVICE (default) or TD_ENGINE_HOST */
+    int64_t start_iter;     /* first iteration index (resume from a checkpoint); <= 0 means 1 */
+} td_chain_params;
+
+/* Engines: DEVICE runs the whole loop (proposal, incremental forward model,
+ * accept/reject) inside one persistent GPU workgroup per td_chain_run call;
+ * HOST is the reference's structure -- every proposal is a full td_evaluate
+ * of the proposed model (TD_inversion_function.jl:93,141,191,238) -- kept as
+ * the parity reference for the DEVICE engine. */
+#define TD_ENGINE_DEVICE 0
+#define TD_ENGINE_HOST 1
+
+typedef struct td_chain_stats {
+    int64_t iterations;        /* proposals drawn so far */
+    int64_t evaluations;       /* forward-model evaluations performed */
+    int64_t accepted[5];       /* per action 1..4 (index 0 unused) */
+    int64_t proposed[5];
+    double phi;                /* current model */
+    int64_t ncells;
+    int64_t bytes;             /* DEVICE engine: algorithmic global-memory bytes read by the proposals */
+} td_chain_stats;
+
+/* Start a chain from the given model (cells may be NULL/0 to draw a starting
+ * model as build_starting, MCsub.jl:76-121). */
+int td_chain_create(td_chain **out, td_ctx *ctx, const td_chain_params *params, const double *xCell,
+                    const double *yCell, const double *zCell, const double *zeta, int64_t nCells);
+int td_chain_destroy(td_chain *ch);
+/* Run `iterations` proposals (TD_inversion_function.jl:70-274 loop body). */
+int td_chain_run(td_chain *ch, int64_t iterations);
+int td_chain_stats_get(const td_chain *ch, td_chain_stats *st);
+/* Copy the current model out (cells arrays capacity `cap`; *nCells receives
+ * the count; ptS_out[n] nullable). */
+int td_chain_get_model(const td_chain *ch, double *xCell, double *yCell, double *zCell, double *zeta,
+                       int64_t cap, int64_t *nCells, double *phi, double *ptS_out);
+/* Tempering: change the temperature between runs (swap step). */
+int td_chain_set_temperature(td_chain *ch, double temperature);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TDSTAR_H */

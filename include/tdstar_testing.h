@@ -1,0 +1,38 @@
+/*
+ * tdstar_testing.h -- host-only hooks of libtdstar.so that expose the chain's
+ * RNG, deterministic math and proposal/acceptance logic (csrc/chain_logic.h)
+ * so the CPU test suite can check them without a GPU.  They compute exactly
+ * what the device kernel computes (same source, __host__ __device__).
+ * Not part of the drop-in boundary; no reference interface is replaced.
+ */
+#ifndef TDSTAR_TESTING_H
+#define TDSTAR_TESTING_H
+#include <stdint.h>
+
+#include "tdstar.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Philox4x32-10 block (Salmon et al. 2011; Random123 known-answer vectors). */
+void tdt_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+double tdt_det_log(double x);
+double tdt_det_exp(double x);
+/* Wichura AS241 standard-normal quantile. */
+double tdt_normal_quantile(double p);
+/* The 7 uniforms of one iteration: action, accept, a, b, c, zeta, index. */
+void tdt_draws(uint64_t seed, uint32_t chain, uint64_t iter, double out[7]);
+/* Proposal of iteration `iter` for the given model (TD_inversion_function.jl:72-236):
+ * out = {action, active, valid, index, x, y, z, zeta}; czeta_birth is the
+ * Interpolation value at the birth site (needed to draw zetanew). */
+int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const double *cx, const double *cy,
+                const double *cz, const double *czeta, double czeta_birth, double out[8]);
+/* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
+int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
+               double phi_n, double czeta, double zeta_killed, double zetanew_death);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

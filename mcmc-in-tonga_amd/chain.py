@@ -1,0 +1,186 @@
+"""rj-MCMC chain -- mirror of TD_inversion_function.jl over the td_chain ABI.
+
+``Chain`` wraps one ``td_chain`` (device-resident loop by default, or the
+HOST engine that calls the full ``td_evaluate`` for every proposal exactly as
+the reference does).  ``TD_inversion_function(TD_parameters, dataStruct,
+chain)`` keeps the reference's signature and bookkeeping: burn-in, thinning
+into ``model_hist`` (copies, not the aliased references the reference
+pushes, TD_inversion_function.jl:280), progress lines every ``print_each``,
+and optional checkpoint/resume (npz, TD_inversion_function.jl:41-67,282-294).
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import TdChainParams, TdChainStats, check, f64, lib, ptr
+from .data import box
+from .defstruct import Model
+from .forward import context_for
+
+ACTIONS = {1: "birth", 2: "death", 3: "change", 4: "move"}
+
+
+def chain_params(TD_parameters, dataStruct=None, seed=1, chain=1, temperature=1.0, engine=_lib.TD_ENGINE_DEVICE,
+                 extent=None):
+    p = TdChainParams()
+    p.debug_prior = int(TD_parameters.debug_prior)
+    p.sig = int(TD_parameters.sig)
+    p.zeta_scale = int(TD_parameters.zeta_scale)
+    p.max_cells = int(TD_parameters.max_cells)
+    p.min_cells = int(TD_parameters.min_cells)
+    p.prior = int(TD_parameters.prior)
+    p.n_iter, p.burn_in, p.keep_each = float(TD_parameters.n_iter), float(TD_parameters.burn_in), \
+        float(TD_parameters.keep_each)
+    if extent is None:
+        if dataStruct is not None:  # min(xVec...), max(xVec...) (TD_inversion_function.jl:30-32)
+            extent = (float(np.min(dataStruct.xVec)), float(np.max(dataStruct.xVec)),
+                      float(np.min(dataStruct.yVec)), float(np.max(dataStruct.yVec)),
+                      float(np.min(dataStruct.zVec)), float(np.max(dataStruct.zVec)))
+        else:
+            extent = box()
+    p.xmin, p.xmax, p.ymin, p.ymax, p.zmin, p.zmax = extent
+    p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    p.chain = int(chain)
+    p.temperature = float(temperature)
+    p.engine = int(engine)
+    return p
+
+
+class Chain:
+    def __init__(self, ctx, params, model=None):
+        self.ctx = ctx
+        self.params = params
+        h = ctypes.c_void_p()
+        if model is not None:
+            cells = [f64(c) for c in model.cells()]
+            check(lib().td_chain_create(ctypes.byref(h), ctx.h, ctypes.byref(params), *(ptr(c) for c in cells),
+                                        len(cells[0])), ctx.h)
+        else:
+            check(lib().td_chain_create(ctypes.byref(h), ctx.h, ctypes.byref(params), None, None, None, None, 0),
+                  ctx.h)
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().td_chain_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, iterations):
+        check(lib().td_chain_run(self.h, int(iterations)), self.ctx.h)
+
+    def stats(self):
+        s = TdChainStats()
+        check(lib().td_chain_stats_get(self.h, ctypes.byref(s)), self.ctx.h)
+        return dict(iterations=s.iterations, evaluations=s.evaluations, accepted=list(s.accepted)[1:],
+                    proposed=list(s.proposed)[1:], phi=s.phi, ncells=s.ncells, bytes=s.bytes)
+
+    def model(self):
+        cap = max(int(self.params.max_cells), self.stats()["ncells"]) + 1
+        arrs = [np.zeros(cap) for _ in range(4)]
+        n = ctypes.c_int64()
+        phi = ctypes.c_double()
+        ptS = np.zeros(max(self.ctx.n, 1))
+        check(lib().td_chain_get_model(self.h, *(ptr(a) for a in arrs), cap, ctypes.byref(n), ctypes.byref(phi),
+                                       ptr(ptS)), self.ctx.h)
+        k = n.value
+        m = Model(float(k), arrs[0][:k].copy(), arrs[1][:k].copy(), arrs[2][:k].copy(), arrs[3][:k].copy())
+        m.phi = phi.value
+        m.ptS = ptS[:self.ctx.n].copy()
+        return m
+
+    def set_temperature(self, T):
+        check(lib().td_chain_set_temperature(self.h, float(T)), self.ctx.h)
+
+
+def build_starting(TD_parameters, dataStruct, seed=1, chain=1):
+    """MCsub.jl:76-121 (log-uniform nCells, uniform cells, zeta ~ U(0, zeta_scale)),
+    drawn by the chain's RNG; returns (model, dataStruct, valid)."""
+    ctx = context_for(dataStruct)
+    ch = Chain(ctx, chain_params(TD_parameters, dataStruct, seed=seed, chain=chain))
+    m = ch.model()
+    ch.close()
+    m.tS = dataStruct.tS
+    m.likelihood = ctx.likelihood_const if TD_parameters.debug_prior != 1 else 1.0
+    return m, dataStruct, 1
+
+
+def TD_inversion_function(TD_parameters, dataStruct, chain, seed=None, model=None, engine=_lib.TD_ENGINE_DEVICE,  # noqa: N802
+                          checkpoint_dir=None, verbose=False, temperature=1.0):
+    """TD_inversion_function.jl:7-305: one chain; returns model_hist (list of Model copies)."""
+    ctx = context_for(dataStruct)
+    seed = chain * 7919 + 1 if seed is None else seed
+    prm = chain_params(TD_parameters, dataStruct, seed=seed, chain=chain, temperature=temperature, engine=engine)
+    n_iter, burn_in, keep = int(TD_parameters.n_iter), int(TD_parameters.burn_in), int(TD_parameters.keep_each)
+    print_each = int(TD_parameters.print_each)
+    num_models = int((TD_parameters.n_iter - TD_parameters.burn_in) / TD_parameters.keep_each)
+    model_hist, it0 = [], 1
+    ckpt = _latest_checkpoint(checkpoint_dir, chain) if checkpoint_dir else None
+    if ckpt is not None:  # :41-67 resume
+        z = np.load(ckpt, allow_pickle=False)
+        model = Model(float(len(z["xCell"])), z["xCell"], z["yCell"], z["zCell"], z["zeta"])
+        it0 = int(z["iter"]) + 1
+        prm.seed = int(z["seed"])
+        for k in range(int(z["n_hist"])):
+            o = z["hist_off"]
+            sl = slice(o[k], o[k + 1])
+            model_hist.append(Model(float(o[k + 1] - o[k]), z["hx"][sl], z["hy"][sl], z["hz"][sl], z["hzeta"][sl],
+                                    phi=float(z["hphi"][k])))
+    prm.start_iter = it0  # the counter-based RNG continues exactly where the checkpoint stopped
+    ch = Chain(ctx, prm, model)
+    model_num = 0
+    it = it0
+    while it <= n_iter:
+        # run up to the next bookkeeping point in one device launch
+        nxt = n_iter
+        if it < burn_in:
+            nxt = min(nxt, burn_in)
+        else:
+            nxt = min(nxt, it + (keep - 1 - (it - burn_in) % keep) if keep > 0 else n_iter)
+        if print_each > 0:
+            nxt = min(nxt, ((it + print_each - 1) // print_each) * print_each)
+        nxt = max(nxt, it)
+        ch.run(nxt - it + 1)
+        it_done = nxt
+        if it_done >= burn_in:
+            model_num = it_done - burn_in + 1
+            if keep > 0 and model_num % keep == 0:
+                m = ch.model()
+                m.tS = dataStruct.tS
+                m.likelihood = ctx.likelihood_const
+                model_hist.append(m)
+                if checkpoint_dir and (len(model_hist) == 1 or (100 * len(model_hist) / max(num_models, 1)) % 10 < 1e-9):
+                    _save_checkpoint(checkpoint_dir, chain, it_done, n_iter, m, model_hist, prm.seed)
+        if verbose and print_each > 0 and it_done % print_each == 0:
+            print("Chain #%d at %g%% with a phi of %r" % (chain, 100 * it_done / n_iter, ch.stats()["phi"]))
+        it = it_done + 1
+    ch.close()
+    return model_hist
+
+
+def _latest_checkpoint(d, chain):
+    # exact chain prefix (the reference's glob("chain1*") also matches chain10..., :41)
+    files = sorted(glob.glob(os.path.join(d, "chain%d_iter*.npz" % chain)),
+                   key=lambda f: int(os.path.basename(f).split("_iter")[1].split("_")[0]))
+    return files[-1] if files else None
+
+
+def _save_checkpoint(d, chain, it, n_iter, model, hist, seed):
+    os.makedirs(d, exist_ok=True)
+    off = np.concatenate([[0], np.cumsum([len(m.xCell) for m in hist])]).astype(np.int64)
+    path = os.path.join(d, "chain%d_iter%d_%g%%.npz" % (chain, it, 100 * it / n_iter))
+    np.savez(path, xCell=model.xCell, yCell=model.yCell, zCell=model.zCell, zeta=model.zeta, iter=it, seed=seed,
+             n_hist=len(hist), hist_off=off, hx=np.concatenate([m.xCell for m in hist]),
+             hy=np.concatenate([m.yCell for m in hist]), hz=np.concatenate([m.zCell for m in hist]),
+             hzeta=np.concatenate([m.zeta for m in hist]), hphi=np.array([m.phi for m in hist]))
+    for f in glob.glob(os.path.join(d, "chain%d_iter*.npz" % chain)):  # keep the newest only (:53-55)
+        if f != path:
+            os.remove(f)

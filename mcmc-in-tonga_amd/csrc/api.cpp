@@ -1,0 +1,435 @@
+// api.cpp -- C ABI of libtdstar (include/tdstar.h): context, evaluate,
+// interpolate.  Host-side glue only; the arithmetic is in kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ctx.h"
+
+namespace {
+thread_local std::string g_err;  // td_create failures (no ctx yet)
+}
+
+namespace tdstar {
+
+int set_err(td_ctx *ctx, int code, const std::string &msg) {
+    if (ctx)
+        ctx->err = msg;
+    else
+        g_err = msg;
+    return code;
+}
+
+int hip_err(td_ctx *ctx, hipError_t e, const char *what) {
+    std::string m = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+    return set_err(ctx, TD_ERR_HIP, m);
+}
+
+#define TD_HIP(ctx, call)                                 \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hip_err(ctx, e_, #call); \
+    } while (0)
+
+// Julia 1.5 Base.sum(::Vector{Float64}) association: n < 16 sequential;
+// otherwise pairwise over 1024-blocks, each block v=a1+a2 then 4 x 8-lane
+// accumulators + sequential tail (oracle/README.md for how this was pinned).
+static double julia_block(const double *a, int64_t f, int64_t l) {
+    if (f == l) return a[f];
+    double v = a[f] + a[f + 1];
+    const int64_t T = l - f - 1, Q = T >= 32 ? T / 32 : 0;
+    int64_t i = f + 2;
+    if (Q > 0) {
+        double acc[32] = {0.0};
+        acc[0] = v;
+        for (int64_t q = 0; q < Q; ++q)
+            for (int k = 0; k < 32; ++k) acc[k] = acc[k] + a[i + q * 32 + k];
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = acc[j];
+        for (int k = 1; k < 4; ++k)
+            for (int j = 0; j < 8; ++j) r[j] = acc[k * 8 + j] + r[j];
+        for (int h = 4; h >= 1; h >>= 1)
+            for (int j = 0; j < h; ++j) r[j] = r[j] + r[j + h];
+        v = r[0];
+        i += Q * 32;
+    }
+    for (; i <= l; ++i) v = v + a[i];
+    return v;
+}
+static double julia_pairwise(const double *a, int64_t f, int64_t l) {
+    if (l - f < 1024) return julia_block(a, f, l);
+    const int64_t mid = f + ((l - f) >> 1);
+    const double v1 = julia_pairwise(a, f, mid);
+    return v1 + julia_pairwise(a, mid + 1, l);
+}
+double julia_sum(const double *a, int64_t n) {
+    if (n == 0) return 0.0;
+    if (n == 1) return a[0];
+    if (n < 16) {
+        double s = a[0] + a[1];
+        for (int64_t i = 2; i < n; ++i) s = s + a[i];
+        return s;
+    }
+    return julia_pairwise(a, 0, n - 1);
+}
+
+// MCsub.jl:179: sum(-log.(allSig * sqrt(2 * pi)) * length(tS)).  Line 180 is a
+// separate statement in Julia, so the Gaussian term is NOT part of it.
+double likelihood_constant(const double *sig, int64_t n) {
+    std::vector<double> t((size_t)n);
+    const volatile double two_pi = 2.0 * 3.141592653589793;
+    const double c = std::sqrt((double)two_pi);
+    for (int64_t k = 0; k < n; ++k) t[(size_t)k] = (-std::log(sig[k] * c)) * (double)n;
+    return julia_sum(t.data(), n);
+}
+
+int ensure_cells(td_ctx *ctx, int64_t ncells) {
+    if (ncells <= ctx->cell_cap && ctx->cells) return TD_OK;
+    int64_t cap = ctx->cell_cap > 0 ? ctx->cell_cap : 256;
+    while (cap < ncells) cap *= 2;
+    if (ctx->cells) (void)hipFree(ctx->cells);
+    if (ctx->h_cells) (void)hipHostFree(ctx->h_cells);
+    ctx->cells = nullptr;
+    ctx->h_cells = nullptr;
+    ctx->cell_cap = 0;
+    TD_HIP(ctx, hipMalloc(&ctx->cells, sizeof(double) * 4 * (size_t)cap));
+    TD_HIP(ctx, hipHostMalloc(&ctx->h_cells, sizeof(double) * 4 * (size_t)cap, hipHostMallocDefault));
+    ctx->cell_cap = cap;
+    return TD_OK;
+}
+
+int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                 int64_t ncells) {
+    int rc = ensure_cells(ctx, ncells);
+    if (rc) return rc;
+    if (ncells == 0) return TD_OK;
+    const int64_t s = ctx->cell_cap;
+    double *h = ctx->h_cells;
+    std::memcpy(h, x, sizeof(double) * (size_t)ncells);
+    std::memcpy(h + s, y, sizeof(double) * (size_t)ncells);
+    std::memcpy(h + 2 * s, z, sizeof(double) * (size_t)ncells);
+    std::memcpy(h + 3 * s, zeta, sizeof(double) * (size_t)ncells);
+    // four slices of the SoA (one copy if the set fills the capacity)
+    for (int k = 0; k < 4; ++k)
+        TD_HIP(ctx, hipMemcpyAsync(ctx->cells + k * s, h + k * s, sizeof(double) * (size_t)ncells,
+                                   hipMemcpyHostToDevice, ctx->stream));
+    return TD_OK;
+}
+
+}  // namespace tdstar
+
+using namespace tdstar;
+
+namespace {
+
+void free_ctx(td_ctx *c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->timer.release();
+    void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->cells,
+                   c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->ptS, c->phi,
+                   c->q, c->q_i, c->q_z};
+    for (void *p : dev)
+        if (p) (void)hipFree(p);
+    void *host[] = {c->h_cells, c->h_out, c->h_best_i, c->h_q, c->h_q_i, c->h_q_z};
+    for (void *p : host)
+        if (p) (void)hipHostFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int64_t leading_non_nan(const double *a, int64_t len) {
+    for (int64_t k = 0; k < len; ++k)
+        if (std::isnan(a[k])) return k;
+    return len;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *td_last_error(const td_ctx *ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, const double *rayZ,
+              const double *rayL, const double *rayU, int64_t m, int64_t n, const double *tS,
+              const double *allSig) {
+    if (!out) return set_err(nullptr, TD_ERR_ARG, "td_create: out is NULL");
+    *out = nullptr;
+    if (m < 1 || n < 0) return set_err(nullptr, TD_ERR_ARG, "td_create: need m >= 1 and n >= 0");
+    if (n > 0 && (!rayX || !rayY || !rayZ || !tS || !allSig || (m > 1 && (!rayL || !rayU))))
+        return set_err(nullptr, TD_ERR_ARG, "td_create: NULL array");
+
+    // ---- validate the NaN layout and build the CSR geometry on the host ----
+    std::vector<int> off((size_t)n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t np = leading_non_nan(rayX + i * m, m);                    // MCsub.jl:312-316
+        const int64_t nl = m > 1 ? leading_non_nan(rayL + i * (m - 1), m - 1) : 0;  // MCsub.jl:150
+        const int64_t want = np > 0 ? np - 1 : 0;
+        if (nl != want) {
+            char buf[200];
+            std::snprintf(buf, sizeof buf,
+                          "td_create: ray %lld has %lld points but %lld leading non-NaN rayL entries "
+                          "(expected %lld; Julia would throw DimensionMismatch)",
+                          (long long)(i + 1), (long long)np, (long long)nl, (long long)want);
+            return set_err(nullptr, TD_ERR_LAYOUT, buf);
+        }
+        off[(size_t)i + 1] = off[(size_t)i] + (int)np;
+        if ((int64_t)off[(size_t)i + 1] > (int64_t)0x7fffffff)
+            return set_err(nullptr, TD_ERR_ARG, "td_create: more than 2^31 points");
+    }
+    const int64_t P = off[(size_t)n];
+    std::vector<double> hx((size_t)P), hy((size_t)P), hz((size_t)P), hw((size_t)P, 0.0);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t b = off[(size_t)i], np = off[(size_t)i + 1] - b;
+        for (int64_t k = 0; k < np; ++k) {
+            hx[(size_t)(b + k)] = rayX[i * m + k];
+            hy[(size_t)(b + k)] = rayY[i * m + k];
+            hz[(size_t)(b + k)] = rayZ[i * m + k];
+            if (k + 1 < np)  // (rayl .* rayu)[k]: first product of MCsub.jl:153/159
+                hw[(size_t)(b + k)] = rayL[i * (m - 1) + k] * rayU[i * (m - 1) + k];
+        }
+    }
+
+    td_ctx *c = new (std::nothrow) td_ctx();
+    if (!c) return set_err(nullptr, TD_ERR_NOMEM, "td_create: out of host memory");
+    auto fail = [&](int code) {
+        g_err = c->err;
+        free_ctx(c);
+        return code;
+    };
+    hipError_t e;
+    if (device < 0) {
+        e = hipGetDevice(&device);
+        if (e != hipSuccess) return fail(hip_err(c, e, "hipGetDevice"));
+    }
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(hip_err(c, e, "hipSetDevice"));
+    c->device = device;
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return fail(hip_err(c, e, "hipGetDeviceProperties"));
+    c->num_cus = prop.multiProcessorCount;
+    c->arch = prop.gcnArchName;
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return fail(hip_err(c, e, "hipStreamCreate"));
+
+    c->g.m = m;
+    c->g.n = n;
+    c->g.P = P;
+    c->ray_off_host = off;
+    c->hx = hx;
+    c->hy = hy;
+    c->hz = hz;
+    c->sig_host.assign(allSig ? allSig : nullptr, allSig ? allSig + n : nullptr);
+    c->likelihood = likelihood_constant(c->sig_host.data(), n);
+
+    auto dalloc = [&](void **p, size_t bytes, const char *what) -> int {
+        hipError_t er = hipMalloc(p, bytes ? bytes : 8);
+        return er == hipSuccess ? TD_OK : hip_err(c, er, what);
+    };
+    const size_t Pb = sizeof(double) * (size_t)(P > 0 ? P : 1);
+    const size_t nb = sizeof(double) * (size_t)(n > 0 ? n : 1);
+    int rc = TD_OK;
+    rc = rc ? rc : dalloc((void **)&c->g.px, Pb, "hipMalloc(px)");
+    rc = rc ? rc : dalloc((void **)&c->g.py, Pb, "hipMalloc(py)");
+    rc = rc ? rc : dalloc((void **)&c->g.pz, Pb, "hipMalloc(pz)");
+    rc = rc ? rc : dalloc((void **)&c->g.w, Pb, "hipMalloc(w)");
+    rc = rc ? rc : dalloc((void **)&c->g.ray_off, sizeof(int) * (size_t)(n + 1), "hipMalloc(ray_off)");
+    rc = rc ? rc : dalloc((void **)&c->g.tS, nb, "hipMalloc(tS)");
+    rc = rc ? rc : dalloc((void **)&c->g.sig, nb, "hipMalloc(sig)");
+    rc = rc ? rc : dalloc((void **)&c->best_i, sizeof(int) * (size_t)(P > 0 ? P : 1), "hipMalloc(best_i)");
+    rc = rc ? rc : dalloc((void **)&c->best_d, Pb, "hipMalloc(best_d)");
+    rc = rc ? rc : dalloc((void **)&c->zeta0, Pb, "hipMalloc(zeta0)");
+    rc = rc ? rc : dalloc((void **)&c->ptS, nb, "hipMalloc(ptS)");
+    rc = rc ? rc : dalloc((void **)&c->phi, sizeof(double), "hipMalloc(phi)");
+    if (rc) return fail(rc);
+    e = hipHostMalloc(&c->h_out, sizeof(double) * (size_t)(n + 1), hipHostMallocDefault);
+    if (e != hipSuccess) return fail(hip_err(c, e, "hipHostMalloc(out)"));
+    e = hipHostMalloc(&c->h_best_i, sizeof(int) * (size_t)(P > 0 ? P : 1), hipHostMallocDefault);
+    if (e != hipSuccess) return fail(hip_err(c, e, "hipHostMalloc(best_i)"));
+
+    struct Up { void *d; const void *h; size_t b; } ups[] = {
+        {c->g.px, hx.data(), sizeof(double) * (size_t)P}, {c->g.py, hy.data(), sizeof(double) * (size_t)P},
+        {c->g.pz, hz.data(), sizeof(double) * (size_t)P}, {c->g.w, hw.data(), sizeof(double) * (size_t)P},
+        {c->g.ray_off, off.data(), sizeof(int) * (size_t)(n + 1)},
+        {c->g.tS, tS, sizeof(double) * (size_t)n}, {c->g.sig, allSig, sizeof(double) * (size_t)n}};
+    for (auto &u : ups)
+        if (u.b) {
+            e = hipMemcpy(u.d, u.h, u.b, hipMemcpyHostToDevice);
+            if (e != hipSuccess) return fail(hip_err(c, e, "hipMemcpy(geometry)"));
+        }
+    rc = ensure_cells(c, 256);
+    if (rc) return fail(rc);
+    *out = c;
+    return TD_OK;
+}
+
+int td_destroy(td_ctx *ctx) {
+    free_ctx(ctx);
+    return TD_OK;
+}
+
+int td_get_info(const td_ctx *ctx, td_info *info) {
+    if (!ctx || !info) return set_err(const_cast<td_ctx *>(ctx), TD_ERR_ARG, "td_get_info: NULL");
+    std::memset(info, 0, sizeof *info);
+    info->abi_version = TDSTAR_ABI_VERSION;
+    info->device = ctx->device;
+    info->m = ctx->g.m;
+    info->n = ctx->g.n;
+    info->npoints = ctx->g.P;
+    int64_t nonempty = 0;
+    for (int64_t i = 0; i < ctx->g.n; ++i) nonempty += ctx->ray_off_host[(size_t)i + 1] > ctx->ray_off_host[(size_t)i];
+    info->nsegments = ctx->g.P - nonempty;
+    info->likelihood = ctx->likelihood;
+    std::snprintf(info->arch, sizeof info->arch, "%s", ctx->arch.c_str());
+    return TD_OK;
+}
+
+int td_set_sigma(td_ctx *ctx, const double *allSig) {
+    if (!ctx || (!allSig && ctx->g.n > 0)) return set_err(ctx, TD_ERR_ARG, "td_set_sigma: NULL");
+    TD_HIP(ctx, hipSetDevice(ctx->device));
+    ctx->sig_host.assign(allSig, allSig + ctx->g.n);
+    ctx->likelihood = likelihood_constant(allSig, ctx->g.n);
+    if (ctx->g.n)
+        TD_HIP(ctx, hipMemcpy(ctx->g.sig, allSig, sizeof(double) * (size_t)ctx->g.n, hipMemcpyHostToDevice));
+    return TD_OK;
+}
+
+int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const double *zCell,
+                const double *zeta, int64_t nCells, int debug_prior, double *ptS_out, double *phi_out,
+                double *likelihood_out, int32_t *nearest_out) {
+    if (!ctx) return set_err(nullptr, TD_ERR_ARG, "td_evaluate: ctx is NULL");
+    if (debug_prior == 1) {  // MCsub.jl:128-136
+        if (phi_out) *phi_out = 1.0;
+        if (likelihood_out) *likelihood_out = 1.0;
+        return TD_OK;
+    }
+    if (nCells < 0 || (nCells > 0 && (!xCell || !yCell || !zCell || !zeta)))
+        return set_err(ctx, TD_ERR_ARG, "td_evaluate: bad cell arrays");
+    if (nCells > 0x7fffffff) return set_err(ctx, TD_ERR_ARG, "td_evaluate: too many cells");
+    TD_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = upload_cells(ctx, xCell, yCell, zCell, zeta, nCells);
+    if (rc) return rc;
+    const auto &g = ctx->g;
+    Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
+    hipError_t e = launch_nearest(g.px, g.py, g.pz, g.P, 1, 1, ctx->cells, ctx->cell_cap, nCells, ctx->nn,
+                                  ctx->num_cus, ctx->best_i, ctx->best_d, ctx->zeta0, ctx->stream, tm);
+    if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
+    e = launch_ray_sums(g, ctx->zeta0, ctx->ptS, ctx->stream, tm);
+    if (e != hipSuccess) return hip_err(ctx, e, "ray-sum kernel");
+    e = launch_chi2(g, ctx->ptS, ctx->phi, ctx->stream, tm);
+    if (e != hipSuccess) return hip_err(ctx, e, "chi2 kernel");
+    TD_HIP(ctx, hipMemcpyAsync(ctx->h_out, ctx->phi, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (g.n)
+        TD_HIP(ctx, hipMemcpyAsync(ctx->h_out + 1, ctx->ptS, sizeof(double) * (size_t)g.n, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    if (nearest_out && g.P)
+        TD_HIP(ctx, hipMemcpyAsync(ctx->h_best_i, ctx->best_i, sizeof(int) * (size_t)g.P, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    TD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (phi_out) *phi_out = ctx->h_out[0];
+    if (ptS_out && g.n) std::memcpy(ptS_out, ctx->h_out + 1, sizeof(double) * (size_t)g.n);
+    if (nearest_out && g.P) std::memcpy(nearest_out, ctx->h_best_i, sizeof(int) * (size_t)g.P);
+    if (likelihood_out) *likelihood_out = ctx->likelihood;  // MCsub.jl:179-182: model-independent
+    return TD_OK;
+}
+
+int td_evaluate_batch(td_ctx *ctx, int64_t nmodels, const int64_t *cell_off, const double *xCell,
+                      const double *yCell, const double *zCell, const double *zeta, double *ptS_out,
+                      double *phi_out, double *likelihood_out) {
+    if (!ctx) return set_err(nullptr, TD_ERR_ARG, "td_evaluate_batch: ctx is NULL");
+    if (nmodels < 0 || (nmodels > 0 && !cell_off)) return set_err(ctx, TD_ERR_ARG, "td_evaluate_batch: bad offsets");
+    for (int64_t k = 0; k < nmodels; ++k) {
+        const int64_t a = cell_off[k], b = cell_off[k + 1];
+        if (b < a || a < 0) return set_err(ctx, TD_ERR_ARG, "td_evaluate_batch: offsets not monotone");
+        int rc = td_evaluate(ctx, xCell ? xCell + a : nullptr, yCell ? yCell + a : nullptr,
+                             zCell ? zCell + a : nullptr, zeta ? zeta + a : nullptr, b - a, 0,
+                             ptS_out ? ptS_out + k * ctx->g.n : nullptr, phi_out ? phi_out + k : nullptr,
+                             likelihood_out ? likelihood_out + k : nullptr, nullptr);
+        if (rc) return rc;
+    }
+    return TD_OK;
+}
+
+int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const double *zCell,
+                   const double *zeta, int64_t nCells, const double *X, int64_t nx, const double *Y,
+                   int64_t ny, const double *Z, int64_t nz, double *zeta_out, int32_t *nearest_out,
+                   int64_t *npoints_out) {
+    if (!ctx) return set_err(nullptr, TD_ERR_ARG, "td_interpolate: ctx is NULL");
+    if (nx < 0 || (nx > 0 && (!X || !Y || !Z || !zeta_out)) || nCells < 0 ||
+        (nCells > 0 && (!xCell || !yCell || !zCell || !zeta)))
+        return set_err(ctx, TD_ERR_ARG, "td_interpolate: bad arguments");
+    const int64_t np = leading_non_nan(X, nx);  // MCsub.jl:312-316
+    if (npoints_out) *npoints_out = np;
+    if ((ny != 1 && ny < np) || (nz != 1 && nz < np))
+        return set_err(ctx, TD_ERR_BOUNDS, "td_interpolate: Y/Z shorter than npoints (Julia BoundsError)");
+    if (np == 0) return TD_OK;
+    TD_HIP(ctx, hipSetDevice(ctx->device));
+    if (np > ctx->q_cap) {
+        void *dev[] = {ctx->q, ctx->q_i, ctx->q_z};
+        for (void *p : dev)
+            if (p) (void)hipFree(p);
+        void *host[] = {ctx->h_q, ctx->h_q_i, ctx->h_q_z};
+        for (void *p : host)
+            if (p) (void)hipHostFree(p);
+        ctx->q = ctx->h_q = ctx->q_z = ctx->h_q_z = nullptr;
+        ctx->q_i = ctx->h_q_i = nullptr;
+        ctx->q_cap = 0;
+        int64_t cap = 64;
+        while (cap < np) cap *= 2;
+        TD_HIP(ctx, hipMalloc(&ctx->q, sizeof(double) * 3 * (size_t)cap));
+        TD_HIP(ctx, hipMalloc(&ctx->q_i, sizeof(int) * (size_t)cap));
+        TD_HIP(ctx, hipMalloc(&ctx->q_z, sizeof(double) * (size_t)cap));
+        TD_HIP(ctx, hipHostMalloc(&ctx->h_q, sizeof(double) * 3 * (size_t)cap, hipHostMallocDefault));
+        TD_HIP(ctx, hipHostMalloc(&ctx->h_q_i, sizeof(int) * (size_t)cap, hipHostMallocDefault));
+        TD_HIP(ctx, hipHostMalloc(&ctx->h_q_z, sizeof(double) * (size_t)cap, hipHostMallocDefault));
+        ctx->q_cap = cap;
+    }
+    const int64_t qc = ctx->q_cap;
+    std::memcpy(ctx->h_q, X, sizeof(double) * (size_t)np);
+    std::memcpy(ctx->h_q + qc, Y, sizeof(double) * (size_t)(ny == 1 ? 1 : np));
+    std::memcpy(ctx->h_q + 2 * qc, Z, sizeof(double) * (size_t)(nz == 1 ? 1 : np));
+    TD_HIP(ctx, hipMemcpyAsync(ctx->q, ctx->h_q, sizeof(double) * 3 * (size_t)qc, hipMemcpyHostToDevice, ctx->stream));
+    int rc = upload_cells(ctx, xCell, yCell, zCell, zeta, nCells);
+    if (rc) return rc;
+    hipError_t e = launch_nearest(ctx->q, ctx->q + qc, ctx->q + 2 * qc, np, ny == 1 ? 0 : 1, nz == 1 ? 0 : 1,
+                                  ctx->cells, ctx->cell_cap, nCells, ctx->nn, ctx->num_cus, ctx->q_i, nullptr,
+                                  ctx->q_z, ctx->stream, ctx->timer.on ? &ctx->timer : nullptr);
+    if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
+    TD_HIP(ctx, hipMemcpyAsync(ctx->h_q_z, ctx->q_z, sizeof(double) * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
+    if (nearest_out)
+        TD_HIP(ctx, hipMemcpyAsync(ctx->h_q_i, ctx->q_i, sizeof(int) * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
+    TD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::memcpy(zeta_out, ctx->h_q_z, sizeof(double) * (size_t)np);
+    if (nearest_out) std::memcpy(nearest_out, ctx->h_q_i, sizeof(int) * (size_t)np);
+    return TD_OK;
+}
+
+int td_timing_enable(td_ctx *ctx, int enable) {
+    if (!ctx) return set_err(nullptr, TD_ERR_ARG, "td_timing_enable: ctx is NULL");
+    ctx->timer.on = enable != 0;
+    return TD_OK;
+}
+
+int td_timing_reset(td_ctx *ctx) {
+    if (!ctx) return set_err(nullptr, TD_ERR_ARG, "td_timing_reset: ctx is NULL");
+    ctx->timer.reset();
+    return TD_OK;
+}
+
+int td_timing_get(td_ctx *ctx, const char *kernel, int64_t *launches, double *total_ms) {
+    if (!ctx || !kernel) return set_err(ctx, TD_ERR_ARG, "td_timing_get: NULL argument");
+    hipError_t e = ctx->timer.collect();
+    if (e != hipSuccess) return hip_err(ctx, e, "td_timing_get");
+    auto it = ctx->timer.acc.find(kernel);
+    if (launches) *launches = it == ctx->timer.acc.end() ? 0 : it->second.first;
+    if (total_ms) *total_ms = it == ctx->timer.acc.end() ? 0.0 : it->second.second;
+    return TD_OK;
+}
+
+}  // extern "C"

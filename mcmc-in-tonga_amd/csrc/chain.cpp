@@ -1,0 +1,495 @@
+// chain.cpp -- rj-MCMC chain behind the C ABI (td_chain_*), both engines,
+// plus the host-only testing hooks of include/tdstar_testing.h.
+//
+// TD_ENGINE_HOST mirrors TD_inversion_function.jl:70-274 literally: every
+// proposal builds the proposed model on the host and calls td_evaluate /
+// td_interpolate (the drop-in boundary).  TD_ENGINE_DEVICE runs the same
+// iterations inside k_chain_run (chain_kernels.hip).  Both draw from the same
+// counter-based RNG and share chain_logic.h, so their trajectories agree bit
+// for bit; the HOST engine is the parity reference for the DEVICE one.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/tdstar_testing.h"
+#include "chain_dev.h"
+#include "chain_logic.h"
+#include "ctx.h"
+
+using namespace tdstar;
+
+struct td_chain {
+    td_ctx *ctx = nullptr;
+    td_chain_params prm{};
+    tdchain::Params P{};
+    int engine = TD_ENGINE_DEVICE;
+    // host engine state (also the device engine's mirror after get_model)
+    std::vector<double> x, y, z, zeta;
+    double phi = 0.0;
+    std::vector<double> ptS;
+    int64_t iter = 1;  // Julia: for iter in iter_ind:n_iter, iter_ind = 1
+    td_chain_stats stats{};
+    // device engine
+    DevChain dev{};
+    void *dev_block = nullptr;  // one allocation for every device array
+    ChainScalars *st_dev = nullptr;
+    ChainScalars *st_host = nullptr;  // pinned
+    NNWork nn;
+    std::vector<int> tile_start_host;
+};
+
+namespace {
+
+int chain_err(td_chain *ch, int code, const std::string &m) { return set_err(ch ? ch->ctx : nullptr, code, m); }
+
+tdchain::Params make_params(const td_chain_params &p) {
+    tdchain::Params P{};
+    P.debug_prior = p.debug_prior;
+    P.max_cells = p.max_cells;
+    P.min_cells = p.min_cells;
+    P.zeta_scale = (double)p.zeta_scale;
+    // TD_inversion_function.jl:22: zeta_scale * sig / 100 (Int*Int, then /)
+    P.sig_zeta = (double)(p.zeta_scale * p.sig) / 100.0;
+    P.xmin = p.xmin; P.xmax = p.xmax;
+    P.ymin = p.ymin; P.ymax = p.ymax;
+    P.zmin = p.zmin; P.zmax = p.zmax;
+    // :30-32: (sig / 100) * (max - min)
+    P.xr = ((double)p.sig / 100.0) * (p.xmax - p.xmin);
+    P.yr = ((double)p.sig / 100.0) * (p.ymax - p.ymin);
+    P.zr = ((double)p.sig / 100.0) * (p.zmax - p.zmin);
+    P.temperature = p.temperature > 0.0 ? p.temperature : 1.0;
+    return P;
+}
+
+// build_starting (MCsub.jl:76-121) with the chain's counter-based RNG in a
+// counter range the iterations never use (iteration index 0).
+void build_starting(td_chain *ch) {
+    const tdchain::Params &P = ch->P;
+    const tdchain::Draws d0 = tdchain::draw_iteration(ch->prm.seed, (uint32_t)ch->prm.chain, 0);
+    // :86-87 floor(exp(rand * log(max/min) + log(min)))
+    const double lr = tdchain::det_log((double)P.max_cells / (double)P.min_cells);
+    const int64_t n = (int64_t)std::floor(tdchain::det_exp(d0.u_action * lr + tdchain::det_log((double)P.min_cells)));
+    ch->x.resize((size_t)n);
+    ch->y.resize((size_t)n);
+    ch->z.resize((size_t)n);
+    ch->zeta.resize((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        // slots (2^31 + i) of iteration 0: never drawn by propose()
+        const tdchain::Draws d = tdchain::draw_iteration(ch->prm.seed ^ 0x5bd1e995ull, (uint32_t)ch->prm.chain,
+                                                         (uint64_t)i);
+        ch->x[(size_t)i] = P.xmin + (P.xmax - P.xmin) * d.u_a;  // :92-94
+        ch->y[(size_t)i] = P.ymin + (P.ymax - P.ymin) * d.u_b;
+        ch->z[(size_t)i] = P.zmin + (P.zmax - P.zmin) * d.u_c;
+        ch->zeta[(size_t)i] = d.u_zeta * P.zeta_scale;  // :100
+    }
+}
+
+int host_evaluate(td_chain *ch, const std::vector<double> &x, const std::vector<double> &y,
+                  const std::vector<double> &z, const std::vector<double> &zeta, double *phi, double *ptS) {
+    return td_evaluate(ch->ctx, x.data(), y.data(), z.data(), zeta.data(), (int64_t)x.size(),
+                       ch->prm.debug_prior, ptS, phi, nullptr, nullptr);
+}
+
+int host_interp1(td_chain *ch, const std::vector<double> &x, const std::vector<double> &y,
+                 const std::vector<double> &z, const std::vector<double> &zeta, double qx, double qy, double qz,
+                 double *val) {
+    int64_t np = 0;
+    return td_interpolate(ch->ctx, x.data(), y.data(), z.data(), zeta.data(), (int64_t)x.size(), &qx, 1, &qy, 1,
+                          &qz, 1, val, nullptr, &np);
+}
+
+// One iteration of TD_inversion_function.jl:70-274 on the host engine.
+int host_iteration(td_chain *ch) {
+    const tdchain::Params &P = ch->P;
+    const tdchain::Draws dr = tdchain::draw_iteration(ch->prm.seed, (uint32_t)ch->prm.chain, (uint64_t)ch->iter);
+    const int64_t N = (int64_t)ch->x.size();
+    tdchain::Proposal p = tdchain::propose(P, dr, N);
+    ch->iter += 1;
+    ch->stats.iterations += 1;
+    if (!p.active) return TD_OK;
+    ch->stats.proposed[p.action] += 1;
+    double czeta = 0.0, zeta_killed = 0.0, zetanew = 0.0;
+    const size_t k = (size_t)p.index;
+    if (p.action != tdchain::kBirth) {
+        zeta_killed = ch->zeta[k];
+        tdchain::complete_proposal(P, dr, p, ch->x[k], ch->y[k], ch->z[k], ch->zeta[k]);
+    } else {
+        int rc = host_interp1(ch, ch->x, ch->y, ch->z, ch->zeta, p.x, p.y, p.z, &czeta);  // :81
+        if (rc) return rc;
+        tdchain::birth_zeta(P, p, czeta);
+    }
+    if (!p.valid) return TD_OK;
+    std::vector<double> nx = ch->x, ny = ch->y, nz = ch->z, nzeta = ch->zeta;  // modeln = deepcopy(model)
+    switch (p.action) {
+        case tdchain::kBirth:  // :85-88 append!
+            nx.push_back(p.x); ny.push_back(p.y); nz.push_back(p.z); nzeta.push_back(p.zeta);
+            break;
+        case tdchain::kDeath:  // :132-135 deleteat!
+            nx.erase(nx.begin() + (long)k); ny.erase(ny.begin() + (long)k);
+            nz.erase(nz.begin() + (long)k); nzeta.erase(nzeta.begin() + (long)k);
+            break;
+        case tdchain::kChange: nzeta[k] = p.zeta; break;  // :189
+        case tdchain::kMove: nx[k] = p.x; ny[k] = p.y; nz[k] = p.z; break;  // :234-236
+    }
+    double phi_n = 0.0;
+    std::vector<double> ptS_n(ch->ptS.size());
+    int rc = host_evaluate(ch, nx, ny, nz, nzeta, &phi_n, ptS_n.data());
+    if (rc) return rc;
+    ch->stats.evaluations += 1;
+    if (p.action == tdchain::kDeath) {  // :146 zetanew = Interpolation(modeln, killed site)
+        rc = host_interp1(ch, nx, ny, nz, nzeta, ch->x[k], ch->y[k], ch->z[k], &zetanew);
+        if (rc) return rc;
+    }
+    if (tdchain::accept(P, p, N, ch->phi, phi_n, czeta, zeta_killed, zetanew)) {
+        ch->x.swap(nx); ch->y.swap(ny); ch->z.swap(nz); ch->zeta.swap(nzeta);
+        ch->phi = phi_n;
+        ch->ptS.swap(ptS_n);
+        ch->stats.accepted[p.action] += 1;
+    }
+    return TD_OK;
+}
+
+// ---------------------------------------------------------------- device ----
+template <class T>
+T *carve(char *&cur, size_t count) {
+    T *p = reinterpret_cast<T *>(cur);
+    cur += ((count * sizeof(T) + 255) / 256) * 256;
+    return p;
+}
+
+int device_setup(td_chain *ch) {
+    td_ctx *c = ch->ctx;
+    const int64_t P = c->g.P, n = c->g.n;
+    // ---- tiles: <= kTilePts consecutive points of one ray, FP64 bounding boxes ----
+    std::vector<int> tstart, tile_of((size_t)P), pt_ray((size_t)P);
+    for (int64_t r = 0; r < n; ++r) {
+        const int a = c->ray_off_host[(size_t)r], b = c->ray_off_host[(size_t)r + 1];
+        for (int q = a; q < b; ++q) pt_ray[(size_t)q] = (int)r;
+        for (int q = a; q < b; q += kTilePts) tstart.push_back(q);
+    }
+    const int ntiles = (int)tstart.size();
+    tstart.push_back((int)P);
+    std::vector<double> lo(3 * (size_t)ntiles), hi(3 * (size_t)ntiles);
+    for (int t = 0; t < ntiles; ++t) {
+        double l[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, h[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+        for (int q = tstart[(size_t)t]; q < tstart[(size_t)t + 1]; ++q) {
+            tile_of[(size_t)q] = t;
+            const double v[3] = {c->hx[(size_t)q], c->hy[(size_t)q], c->hz[(size_t)q]};
+            for (int a = 0; a < 3; ++a)
+                if (!std::isnan(v[a])) {
+                    l[a] = std::min(l[a], v[a]);
+                    h[a] = std::max(h[a], v[a]);
+                }
+        }
+        for (int a = 0; a < 3; ++a) {
+            lo[(size_t)a * ntiles + t] = l[a];
+            hi[(size_t)a * ntiles + t] = h[a];
+        }
+    }
+    ch->tile_start_host = tstart;
+    const int cap = std::max<int>(ch->prm.max_cells, (int)ch->x.size()) + 1;
+    // ---- one device block for everything the chain owns ----
+    size_t bytes = 0;
+    auto add = [&](size_t b) { bytes += ((b + 255) / 256) * 256; };
+    const size_t Pn = (size_t)std::max<int64_t>(P, 1), nn = (size_t)std::max<int64_t>(n, 1);
+    add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * Pn); add(sizeof(int) * Pn);
+    add(sizeof(double) * 3 * ntiles); add(sizeof(double) * 3 * ntiles); add(sizeof(double) * (ntiles + 1));
+    add(sizeof(double) * 4 * cap); for (int i = 0; i < 4; ++i) add(sizeof(int) * cap);
+    add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn);
+    add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn); add(Pn);
+    add(sizeof(int) * Pn); add(sizeof(int) * Pn); add(sizeof(int) * (ntiles + 1));
+    for (int i = 0; i < 4; ++i) add(sizeof(double) * nn);
+    add(sizeof(int) * nn); add(sizeof(int) * nn); add(sizeof(ChainScalars));
+    hipError_t e = hipMalloc(&ch->dev_block, bytes);
+    if (e != hipSuccess) return hip_err(c, e, "hipMalloc(chain state)");
+    e = hipMemsetAsync(ch->dev_block, 0, bytes, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "hipMemset(chain state)");
+    char *cur = (char *)ch->dev_block;
+    DevChain &d = ch->dev;
+    d.px = c->g.px; d.py = c->g.py; d.pz = c->g.pz; d.w = c->g.w; d.tS = c->g.tS; d.sig = c->g.sig;
+    d.ray_off = c->g.ray_off;
+    d.P = (int)P;
+    d.n = (int)n;
+    int *tile_start = carve<int>(cur, ntiles + 1);
+    int *tile_of_d = carve<int>(cur, Pn);
+    int *pt_ray_d = carve<int>(cur, Pn);
+    double *tlo = carve<double>(cur, 3 * (size_t)ntiles);
+    double *thi = carve<double>(cur, 3 * (size_t)ntiles);
+    d.tile_start = tile_start; d.tile_of = tile_of_d; d.pt_ray = pt_ray_d; d.tile_lo = tlo; d.tile_hi = thi;
+    d.tile_maxd = carve<double>(cur, ntiles + 1);
+    d.ntiles = ntiles;
+    double *cells = carve<double>(cur, 4 * (size_t)cap);
+    d.cx = cells; d.cy = cells + cap; d.cz = cells + 2 * cap; d.czeta = cells + 3 * cap;
+    d.order = carve<int>(cur, cap); d.rank = carve<int>(cur, cap);
+    d.free_slots = carve<int>(cur, cap); d.order_tmp = carve<int>(cur, cap);
+    d.cap = cap;
+    d.best_s = carve<int>(cur, Pn); d.best_d = carve<double>(cur, Pn); d.zeta0 = carve<double>(cur, Pn);
+    d.cand_s = carve<int>(cur, Pn); d.cand_d = carve<double>(cur, Pn); d.cand_z = carve<double>(cur, Pn);
+    d.cand_flag = carve<unsigned char>(cur, Pn);
+    d.changed = carve<int>(cur, Pn); d.orphans = carve<int>(cur, Pn); d.tiles_hit = carve<int>(cur, ntiles + 1);
+    d.ptS = carve<double>(cur, nn); d.cand_ptS = carve<double>(cur, nn);
+    d.prefix = carve<double>(cur, nn); d.cand_prefix = carve<double>(cur, nn);
+    d.rays_hit = carve<int>(cur, nn); d.ray_flag = carve<int>(cur, nn);
+    d.st = carve<ChainScalars>(cur, 1);
+    ch->st_dev = d.st;
+    d.params = ch->P;
+    d.seed = ch->prm.seed;
+    d.chain = (uint32_t)ch->prm.chain;
+
+    e = hipHostMalloc(&ch->st_host, sizeof(ChainScalars), hipHostMallocDefault);
+    if (e != hipSuccess) return hip_err(c, e, "hipHostMalloc(chain scalars)");
+    // ---- uploads ----
+    const int N = (int)ch->x.size();
+    std::vector<int> ident((size_t)cap);
+    for (int i = 0; i < cap; ++i) ident[(size_t)i] = i;
+    std::vector<double> hc(4 * (size_t)cap, 0.0);
+    std::copy(ch->x.begin(), ch->x.end(), hc.begin());
+    std::copy(ch->y.begin(), ch->y.end(), hc.begin() + cap);
+    std::copy(ch->z.begin(), ch->z.end(), hc.begin() + 2 * cap);
+    std::copy(ch->zeta.begin(), ch->zeta.end(), hc.begin() + 3 * cap);
+    ChainScalars s0{};
+    s0.iter = ch->iter;
+    s0.ncells = N;
+    s0.nslots = N;
+    s0.nfree = 0;
+    s0.phi = 1.0;  // debug_prior: evaluate returns phi = 1 (MCsub.jl:131)
+    struct Up { void *d; const void *h; size_t b; } ups[] = {
+        {tile_start, tstart.data(), sizeof(int) * tstart.size()},
+        {tile_of_d, tile_of.data(), sizeof(int) * (size_t)P},
+        {pt_ray_d, pt_ray.data(), sizeof(int) * (size_t)P},
+        {tlo, lo.data(), sizeof(double) * lo.size()},
+        {thi, hi.data(), sizeof(double) * hi.size()},
+        {cells, hc.data(), sizeof(double) * hc.size()},
+        {d.order, ident.data(), sizeof(int) * (size_t)cap},
+        {d.rank, ident.data(), sizeof(int) * (size_t)cap},
+        {d.st, &s0, sizeof s0}};
+    for (auto &u : ups)
+        if (u.b) {
+            e = hipMemcpyAsync(u.d, u.h, u.b, hipMemcpyHostToDevice, c->stream);
+            if (e != hipSuccess) return hip_err(c, e, "hipMemcpy(chain setup)");
+        }
+    if (ch->prm.debug_prior != 1) {
+        e = chain_full_state(d, N, ch->nn, c->num_cus, c->stream);
+        if (e != hipSuccess) return hip_err(c, e, "chain initial evaluate");
+    }
+    e = hipStreamSynchronize(c->stream);  // the host vectors above die here
+    if (e != hipSuccess) return hip_err(c, e, "chain setup sync");
+    return TD_OK;
+}
+
+int device_pull_scalars(td_chain *ch) {
+    td_ctx *c = ch->ctx;
+    hipError_t e = hipMemcpyAsync(ch->st_host, ch->st_dev, sizeof(ChainScalars), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "chain scalars");
+    const ChainScalars &s = *ch->st_host;
+    ch->iter = s.iter;
+    ch->phi = s.phi;
+    ch->stats.evaluations = s.evaluations;
+    for (int a = 0; a < 5; ++a) {
+        ch->stats.accepted[a] = s.accepted[a];
+        ch->stats.proposed[a] = s.proposed[a];
+    }
+    ch->stats.ncells = s.ncells;
+    ch->stats.phi = s.phi;
+    ch->stats.bytes = s.bytes;
+    return TD_OK;
+}
+
+void free_chain(td_chain *ch) {
+    if (!ch) return;
+    if (ch->ctx && ch->ctx->stream) (void)hipStreamSynchronize(ch->ctx->stream);
+    if (ch->dev_block) (void)hipFree(ch->dev_block);
+    if (ch->st_host) (void)hipHostFree(ch->st_host);
+    if (ch->nn.part_d) (void)hipFree(ch->nn.part_d);
+    if (ch->nn.part_i) (void)hipFree(ch->nn.part_i);
+    delete ch;
+}
+
+}  // namespace
+
+extern "C" {
+
+int td_chain_create(td_chain **out, td_ctx *ctx, const td_chain_params *params, const double *xCell,
+                    const double *yCell, const double *zCell, const double *zeta, int64_t nCells) {
+    if (!out || !ctx || !params) return set_err(ctx, TD_ERR_ARG, "td_chain_create: NULL argument");
+    *out = nullptr;
+    const td_chain_params &p = *params;
+    if (p.prior != 1) return set_err(ctx, TD_ERR_ARG, "td_chain_create: only prior == 1 (uniform) is supported");
+    if (p.min_cells < 1 || p.max_cells < p.min_cells || p.sig <= 0 || p.zeta_scale <= 0)
+        return set_err(ctx, TD_ERR_ARG, "td_chain_create: bad cell bounds / sig / zeta_scale");
+    if (!(p.xmax >= p.xmin && p.ymax >= p.ymin && p.zmax >= p.zmin))
+        return set_err(ctx, TD_ERR_ARG, "td_chain_create: empty box");
+    if (p.engine != TD_ENGINE_DEVICE && p.engine != TD_ENGINE_HOST)
+        return set_err(ctx, TD_ERR_ARG, "td_chain_create: unknown engine");
+    if (nCells < 0 || (nCells > 0 && (!xCell || !yCell || !zCell || !zeta)))
+        return set_err(ctx, TD_ERR_ARG, "td_chain_create: bad cell arrays");
+    td_chain *ch = new (std::nothrow) td_chain();
+    if (!ch) return set_err(ctx, TD_ERR_NOMEM, "td_chain_create: out of memory");
+    ch->ctx = ctx;
+    ch->prm = p;
+    ch->P = make_params(p);
+    ch->engine = p.engine;
+    ch->iter = p.start_iter > 0 ? p.start_iter : 1;
+    if (nCells > 0) {
+        ch->x.assign(xCell, xCell + nCells);
+        ch->y.assign(yCell, yCell + nCells);
+        ch->z.assign(zCell, zCell + nCells);
+        ch->zeta.assign(zeta, zeta + nCells);
+    } else {
+        build_starting(ch);
+    }
+    ch->ptS.assign((size_t)ctx->g.n, 0.0);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) {
+        int rc = hip_err(ctx, e, "hipSetDevice");
+        free_chain(ch);
+        return rc;
+    }
+    int rc = TD_OK;
+    if (ch->engine == TD_ENGINE_HOST) {
+        rc = host_evaluate(ch, ch->x, ch->y, ch->z, ch->zeta, &ch->phi, ch->ptS.data());  // build_starting :118
+        if (!rc) ch->stats.evaluations = 1;
+    } else {
+        rc = device_setup(ch);
+        if (!rc) rc = device_pull_scalars(ch);
+        if (!rc) ch->stats.evaluations = 1;
+    }
+    if (rc) {
+        free_chain(ch);
+        return rc;
+    }
+    ch->stats.phi = ch->phi;
+    ch->stats.ncells = (int64_t)ch->x.size();
+    *out = ch;
+    return TD_OK;
+}
+
+int td_chain_destroy(td_chain *ch) {
+    free_chain(ch);
+    return TD_OK;
+}
+
+int td_chain_run(td_chain *ch, int64_t iterations) {
+    if (!ch || iterations < 0) return chain_err(ch, TD_ERR_ARG, "td_chain_run: bad arguments");
+    if (iterations == 0) return TD_OK;
+    hipError_t e = hipSetDevice(ch->ctx->device);
+    if (e != hipSuccess) return hip_err(ch->ctx, e, "hipSetDevice");
+    if (ch->engine == TD_ENGINE_HOST) {
+        for (int64_t i = 0; i < iterations; ++i) {
+            int rc = host_iteration(ch);
+            if (rc) return rc;
+        }
+        ch->stats.phi = ch->phi;
+        ch->stats.ncells = (int64_t)ch->x.size();
+        return TD_OK;
+    }
+    Timer *tm = ch->ctx->timer.on ? &ch->ctx->timer : nullptr;
+    hipEvent_t t0 = tm ? tm->begin(ch->ctx->stream) : nullptr;
+    e = chain_run(ch->dev, iterations, ch->ctx->stream);
+    if (tm) tm->end("chain_run", t0, ch->ctx->stream);
+    if (e != hipSuccess) return hip_err(ch->ctx, e, "k_chain_run launch");
+    const int64_t before = ch->stats.iterations;
+    int rc = device_pull_scalars(ch);
+    ch->stats.iterations = before + iterations;
+    return rc;
+}
+
+int td_chain_stats_get(const td_chain *ch, td_chain_stats *st) {
+    if (!ch || !st) return TD_ERR_ARG;
+    *st = ch->stats;
+    return TD_OK;
+}
+
+int td_chain_get_model(const td_chain *chc, double *xCell, double *yCell, double *zCell, double *zeta, int64_t cap,
+                       int64_t *nCells, double *phi, double *ptS_out) {
+    td_chain *ch = const_cast<td_chain *>(chc);
+    if (!ch) return TD_ERR_ARG;
+    td_ctx *c = ch->ctx;
+    if (ch->engine == TD_ENGINE_DEVICE) {
+        int rc = device_pull_scalars(ch);
+        if (rc) return rc;
+        const int N = ch->st_host->ncells, cp = ch->dev.cap;
+        std::vector<double> hc(4 * (size_t)cp);
+        std::vector<int> order((size_t)std::max(N, 1));
+        hipError_t e = hipMemcpy(hc.data(), ch->dev.cx, sizeof(double) * hc.size(), hipMemcpyDeviceToHost);
+        if (e == hipSuccess && N > 0)
+            e = hipMemcpy(order.data(), ch->dev.order, sizeof(int) * (size_t)N, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && ptS_out && c->g.n)
+            e = hipMemcpy(ch->ptS.data(), ch->dev.ptS, sizeof(double) * (size_t)c->g.n, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_err(c, e, "td_chain_get_model");
+        ch->x.resize((size_t)N); ch->y.resize((size_t)N); ch->z.resize((size_t)N); ch->zeta.resize((size_t)N);
+        for (int j = 0; j < N; ++j) {
+            const int s = order[(size_t)j];
+            ch->x[(size_t)j] = hc[(size_t)s];
+            ch->y[(size_t)j] = hc[(size_t)cp + s];
+            ch->z[(size_t)j] = hc[2 * (size_t)cp + s];
+            ch->zeta[(size_t)j] = hc[3 * (size_t)cp + s];
+        }
+    }
+    const int64_t N = (int64_t)ch->x.size();
+    if (nCells) *nCells = N;
+    if (phi) *phi = ch->phi;
+    if (cap < N) return set_err(c, TD_ERR_ARG, "td_chain_get_model: capacity smaller than nCells");
+    if (xCell) std::copy(ch->x.begin(), ch->x.end(), xCell);
+    if (yCell) std::copy(ch->y.begin(), ch->y.end(), yCell);
+    if (zCell) std::copy(ch->z.begin(), ch->z.end(), zCell);
+    if (zeta) std::copy(ch->zeta.begin(), ch->zeta.end(), zeta);
+    if (ptS_out) std::copy(ch->ptS.begin(), ch->ptS.end(), ptS_out);
+    return TD_OK;
+}
+
+int td_chain_set_temperature(td_chain *ch, double temperature) {
+    if (!ch || !(temperature > 0.0)) return chain_err(ch, TD_ERR_ARG, "td_chain_set_temperature: need T > 0");
+    ch->prm.temperature = temperature;
+    ch->P.temperature = temperature;
+    ch->dev.params.temperature = temperature;
+    return TD_OK;
+}
+
+// --------------------------------------------------------- testing hooks ----
+void tdt_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    const tdchain::U4 r = tdchain::philox(tdchain::U4{ctr[0], ctr[1], ctr[2], ctr[3]}, key[0], key[1]);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
+}
+double tdt_det_log(double x) { return tdchain::det_log(x); }
+double tdt_det_exp(double x) { return tdchain::det_exp(x); }
+double tdt_normal_quantile(double p) { return tdchain::normal_quantile(p); }
+void tdt_draws(uint64_t seed, uint32_t chain, uint64_t iter, double out[7]) {
+    const tdchain::Draws d = tdchain::draw_iteration(seed, chain, iter);
+    const double v[7] = {d.u_action, d.u_accept, d.u_a, d.u_b, d.u_c, d.u_zeta, d.u_index};
+    std::memcpy(out, v, sizeof v);
+}
+int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const double *cx, const double *cy,
+                const double *cz, const double *czeta, double czeta_birth, double out[8]) {
+    const tdchain::Params P = make_params(*prm);
+    const tdchain::Draws d = tdchain::draw_iteration(prm->seed, (uint32_t)prm->chain, iter);
+    tdchain::Proposal p = tdchain::propose(P, d, ncells);
+    if (p.active && p.action != tdchain::kBirth) {
+        const size_t k = (size_t)p.index;
+        tdchain::complete_proposal(P, d, p, cx[k], cy[k], cz[k], czeta[k]);
+    } else if (p.active) {
+        tdchain::birth_zeta(P, p, czeta_birth);
+    }
+    const double v[8] = {(double)p.action, (double)p.active, (double)p.valid, (double)p.index, p.x, p.y, p.z, p.zeta};
+    std::memcpy(out, v, sizeof v);
+    return 0;
+}
+int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
+               double phi_n, double czeta, double zeta_killed, double zetanew_death) {
+    const tdchain::Params P = make_params(*prm);
+    tdchain::Proposal p{};
+    p.action = action;
+    p.active = 1;
+    p.valid = 1;
+    p.u_accept = u_accept;
+    p.zeta = zeta_new;
+    return tdchain::accept(P, p, ncells, phi, phi_n, czeta, zeta_killed, zetanew_death) ? 1 : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,306 @@
+// chain_logic.h -- rj-MCMC proposal logic shared by the host chain and the
+// device-resident chain kernel (TD_inversion_function.jl:70-274, prior == 1).
+//
+// Everything here is __host__ __device__ and uses only IEEE +,-,*,/ and
+// sqrt (all correctly rounded on both sides, the TUs are compiled with
+// -ffp-contract=off), so a chain driven from the host and the same chain run
+// inside a GPU kernel draw bit-identical proposals and make identical
+// accept/reject decisions.  That is what the chain parity tests check.
+//
+// RNG: Philox4x32-10 (Salmon et al., SC'11), counter = (iteration, slot,
+// chain), key = seed.  Counter-based, so a proposal's draws depend only on
+// (seed, chain, iteration) -- reproducible, unlike the reference's
+// wall-clock seed (TD_inversion_function.jl:13).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TD_HD __host__ __device__ __forceinline__
+#else
+#define TD_HD __host__ __device__ inline
+#endif
+
+namespace tdchain {
+
+// ------------------------------------------------------------------ RNG ----
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+TD_HD void mulhilo(uint32_t a, uint32_t b, uint32_t &hi, uint32_t &lo) {
+    const uint64_t p = (uint64_t)a * (uint64_t)b;
+    hi = (uint32_t)(p >> 32);
+    lo = (uint32_t)p;
+}
+
+TD_HD U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0, lo0, hi1, lo1;
+        mulhilo(0xD2511F53u, c.x, hi0, lo0);
+        mulhilo(0xCD9E8D57u, c.z, hi1, lo1);
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// 53-bit uniform in (0,1): (k + 0.5) / 2^53, never 0 or 1.
+TD_HD double u01(uint32_t a, uint32_t b) {
+    const uint64_t k = ((uint64_t)a << 21) ^ (uint64_t)(b >> 11);
+    const uint64_t m = k & ((1ull << 53) - 1);
+    return ((double)m + 0.5) * (1.0 / 9007199254740992.0);
+}
+
+// Draw slots of one iteration: each slot is one Philox block = 2 uniforms.
+enum Slot : uint32_t { kSlotAction = 0, kSlotXY = 1, kSlotZZeta = 2, kSlotIndex = 3 };
+
+struct Draws {
+    double u_action, u_accept, u_a, u_b, u_c, u_zeta, u_index;
+};
+
+TD_HD Draws draw_iteration(uint64_t seed, uint32_t chain, uint64_t iter) {
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const uint32_t i0 = (uint32_t)iter, i1 = (uint32_t)(iter >> 32);
+    const U4 a = philox(U4{i0, i1, kSlotAction, chain}, k0, k1);
+    const U4 b = philox(U4{i0, i1, kSlotXY, chain}, k0, k1);
+    const U4 c = philox(U4{i0, i1, kSlotZZeta, chain}, k0, k1);
+    const U4 d = philox(U4{i0, i1, kSlotIndex, chain}, k0, k1);
+    Draws r;
+    r.u_action = u01(a.x, a.y);
+    r.u_accept = u01(a.z, a.w);
+    r.u_a = u01(b.x, b.y);
+    r.u_b = u01(b.z, b.w);
+    r.u_c = u01(c.x, c.y);
+    r.u_zeta = u01(c.z, c.w);
+    r.u_index = u01(d.x, d.y);
+    return r;
+}
+
+// ------------------------------------------------- deterministic math ----
+TD_HD uint64_t dbits(double x) {
+    union { double d; uint64_t u; } v;
+    v.d = x;
+    return v.u;
+}
+TD_HD double bitsd(uint64_t u) {
+    union { double d; uint64_t u; } v;
+    v.u = u;
+    return v.d;
+}
+
+// natural log for finite x > 0 (atanh series around 1 after exponent split).
+TD_HD double det_log(double x) {
+    if (!(x > 0.0)) return x == 0.0 ? -__builtin_huge_val() : __builtin_nan("");
+    if (x == __builtin_huge_val()) return x;
+    uint64_t u = dbits(x);
+    int e = (int)((u >> 52) & 0x7ff);
+    if (e == 0) {  // subnormal: scale up by 2^54
+        x = x * 18014398509481984.0;
+        u = dbits(x);
+        e = (int)((u >> 52) & 0x7ff) - 54;
+    }
+    e -= 1023;
+    double m = bitsd((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);  // [1,2)
+    if (m > 1.4142135623730951) {
+        m = m * 0.5;
+        e += 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0);
+    const double s2 = s * s;
+    // 2*(s + s^3/3 + ... + s^23/23), |s| < 0.1716
+    double p = 1.0 / 23.0;
+    p = p * s2 + 1.0 / 21.0;
+    p = p * s2 + 1.0 / 19.0;
+    p = p * s2 + 1.0 / 17.0;
+    p = p * s2 + 1.0 / 15.0;
+    p = p * s2 + 1.0 / 13.0;
+    p = p * s2 + 1.0 / 11.0;
+    p = p * s2 + 1.0 / 9.0;
+    p = p * s2 + 1.0 / 7.0;
+    p = p * s2 + 1.0 / 5.0;
+    p = p * s2 + 1.0 / 3.0;
+    p = p * s2 + 1.0;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    return (double)e * ln2_hi + (2.0 * s * p + (double)e * ln2_lo);
+}
+
+TD_HD double det_exp(double x) {
+    if (x != x) return x;
+    if (x > 709.78) return __builtin_huge_val();
+    if (x < -745.2) return 0.0;
+    const double inv_ln2 = 1.4426950408889634;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    double kd = x * inv_ln2;
+    kd = kd >= 0.0 ? (double)(int64_t)(kd + 0.5) : -(double)(int64_t)(-kd + 0.5);
+    const double r = (x - kd * ln2_hi) - kd * ln2_lo;
+    // Taylor to r^13, |r| <= 0.35
+    double p = 1.0 / 6227020800.0;
+    p = p * r + 1.0 / 479001600.0;
+    p = p * r + 1.0 / 39916800.0;
+    p = p * r + 1.0 / 3628800.0;
+    p = p * r + 1.0 / 362880.0;
+    p = p * r + 1.0 / 40320.0;
+    p = p * r + 1.0 / 5040.0;
+    p = p * r + 1.0 / 720.0;
+    p = p * r + 1.0 / 120.0;
+    p = p * r + 1.0 / 24.0;
+    p = p * r + 1.0 / 6.0;
+    p = p * r + 0.5;
+    p = p * r + 1.0;
+    p = p * r + 1.0;
+    int k = (int)kd;
+    // scale by 2^k in two steps to stay in range
+    const int k1 = k / 2, k2 = k - k1;
+    p = p * bitsd((uint64_t)(1023 + k1) << 52);
+    return p * bitsd((uint64_t)(1023 + k2) << 52);
+}
+
+// Standard normal quantile, Wichura AS241 (PPND16), u in (0,1).
+TD_HD double normal_quantile(double p) {
+    const double q = p - 0.5;
+    if ((q < 0 ? -q : q) <= 0.425) {
+        const double r = 0.180625 - q * q;
+        return q * (((((((r * 2509.0809287301226727 + 33430.575583588128105) * r + 67265.770927008700853) * r +
+                         45921.953931549871457) * r + 13731.693765509461125) * r + 1971.5909503065514427) * r +
+                      133.14166789178437745) * r + 3.387132872796366608) /
+               (((((((r * 5226.495278852545925 + 28729.085735721942674) * r + 39307.89580009271061) * r +
+                    21213.794301586595867) * r + 5394.1960214247511077) * r + 687.1870074920579083) * r +
+                 42.313330701600911252) * r + 1.0);
+    }
+    double r = q < 0 ? p : 1.0 - p;
+    r = __builtin_sqrt(-det_log(r));
+    double val;
+    if (r <= 5.0) {
+        r -= 1.6;
+        val = (((((((r * 7.7454501427834140764e-4 + 0.0227238449892691845833) * r + 0.24178072517745061177) * r +
+                   1.27045825245236838258) * r + 3.64784832476320460504) * r + 5.7694972214606914055) * r +
+                4.6303378461565452959) * r + 1.42343711074968357734) /
+              (((((((r * 1.05075007164441684324e-9 + 5.475938084995344946e-4) * r + 0.0151986665636164571966) * r +
+                   0.14810397642748007459) * r + 0.68976733498510000455) * r + 1.6763848301838038494) * r +
+                2.05319162663775882187) * r + 1.0);
+    } else {
+        r -= 5.0;
+        val = (((((((r * 2.01033439929228813265e-7 + 2.71155556874348757815e-5) * r + 0.0012426609473880784386) * r +
+                   0.026532189526576123093) * r + 0.29656057182850489123) * r + 1.7848265399172913358) * r +
+                5.4637849111641143699) * r + 6.6579046435011037772) /
+              (((((((r * 2.04426310338993978564e-15 + 1.4215117583164458887e-7) * r + 1.8463183175100546818e-5) * r +
+                   7.868691311456132591e-4) * r + 0.0148753612908506148525) * r + 0.13692988092273580531) * r +
+                0.59983220655588793769) * r + 1.0);
+    }
+    return q < 0 ? -val : val;
+}
+
+// ------------------------------------------------------ the proposal ----
+enum Action : int { kBirth = 1, kDeath = 2, kChange = 3, kMove = 4 };
+
+struct Params {
+    int debug_prior, max_cells, min_cells;
+    double zeta_scale, sig_zeta;           // sig_zeta = zeta_scale*sig/100 (TD_inversion_function.jl:22)
+    double xmin, xmax, ymin, ymax, zmin, zmax;
+    double xr, yr, zr;                     // (sig/100)*(max-min), :30-32
+    double temperature;
+};
+
+// What the iteration proposes, before any forward-model evaluation.
+struct Proposal {
+    int action;       // 1..4
+    int active;       // 0: branch skipped (nCells at max / min)
+    int valid;        // 0: invalid, no evaluation, rejected
+    int64_t index;    // kill / change / move cell (0-based)
+    double x, y, z;   // birth location / move target
+    double zeta;      // change: new value (birth: filled after czeta is known)
+    double u_zeta;    // birth: uniform for zetanew ~ Normal(czeta, sig_zeta)
+    double u_accept;
+};
+
+// TD_inversion_function.jl:72 (action = rand(1:4)) and the draws of each
+// branch that do not depend on the selected cell.
+TD_HD Proposal propose(const Params &P, const Draws &d, int64_t ncells) {
+    Proposal p{};
+    p.action = 1 + (int)(d.u_action * 4.0);
+    if (p.action > 4) p.action = 4;
+    p.u_accept = d.u_accept;
+    p.u_zeta = d.u_zeta;
+    p.valid = 1;
+    p.active = 1;
+    switch (p.action) {
+        case kBirth:  // :77-80
+            if (ncells >= P.max_cells) { p.active = 0; p.valid = 0; break; }
+            p.x = d.u_a * (P.xmax - P.xmin) + P.xmin;
+            p.y = d.u_b * (P.ymax - P.ymin) + P.ymin;
+            p.z = d.u_c * (P.zmax - P.zmin) + P.zmin;
+            break;
+        case kDeath:  // :127-128 kill = rand(1:nCells)
+            if (ncells <= P.min_cells) { p.active = 0; p.valid = 0; break; }
+            break;
+        case kChange:  // :184 (always active)
+        case kMove:    // :221
+            if (ncells <= 0) { p.active = 0; p.valid = 0; break; }
+            break;
+    }
+    if (p.active && p.action != kBirth) {
+        p.index = (int64_t)(d.u_index * (double)ncells);
+        if (p.index >= ncells) p.index = ncells - 1;
+    }
+    return p;
+}
+
+// The parts that need the selected cell (position p.index): change draws the
+// new zeta (:188, validity :195), move draws the new site (:226-232).
+TD_HD void complete_proposal(const Params &P, const Draws &d, Proposal &p, double cx, double cy, double cz,
+                             double czeta) {
+    if (!p.active) return;
+    if (p.action == kChange) {
+        p.zeta = czeta + P.sig_zeta * normal_quantile(d.u_zeta);
+        p.valid = (p.zeta > 0.0 && p.zeta < P.zeta_scale) ? 1 : 0;
+    } else if (p.action == kMove) {
+        p.x = cx + P.xr * normal_quantile(d.u_a);
+        p.y = cy + P.yr * normal_quantile(d.u_b);
+        p.z = cz + P.zr * normal_quantile(d.u_c);
+        p.zeta = czeta;
+        p.valid = (p.x >= P.xmin && p.x <= P.xmax && p.y >= P.ymin && p.y <= P.ymax && p.z >= P.zmin &&
+                   p.z <= P.zmax) ? 1 : 0;
+    }
+}
+
+// Birth, once czeta = Interpolation(model, xNew, yNew, zNew) is known (:81-82, :92).
+TD_HD void birth_zeta(const Params &P, Proposal &p, double czeta) {
+    p.zeta = czeta + P.sig_zeta * normal_quantile(p.u_zeta);
+    p.valid = (p.zeta > 0.0 && p.zeta < P.zeta_scale) ? 1 : 0;
+}
+
+// log of the acceptance ratio (before min(1, .)), prior == 1 (uniform).
+// extra: birth -> czeta, death -> zetanew = Interpolation(modeln, killed site) (:146)
+TD_HD bool accept(const Params &P, const Proposal &p, int64_t ncells, double phi, double phi_n, double czeta,
+                  double zeta_killed, double zetanew_death) {
+    if (!p.active || !p.valid) return false;
+    const double dphi = (phi_n - phi) / (2.0 * P.temperature);
+    const double two_pi_sqrt = 2.5066282746310002;  // sqrt(2*pi)
+    double alpha;
+    switch (p.action) {
+        case kBirth: {  // eq. 16, :96-97
+            const double N = (double)ncells;
+            const double dz = czeta - p.zeta;
+            alpha = (N / (N + 1.0)) * ((P.sig_zeta * two_pi_sqrt) / P.zeta_scale) *
+                    det_exp((dz * dz) / (2.0 * P.sig_zeta * P.sig_zeta) - dphi);
+            break;
+        }
+        case kDeath: {  // eq. 17, :151-152
+            const double N = (double)ncells;
+            const double dz = zeta_killed - zetanew_death;
+            alpha = (N / (N - 1.0)) * (P.zeta_scale / (P.sig_zeta * two_pi_sqrt)) *
+                    det_exp(-(dz * dz) / (2.0 * P.sig_zeta * P.sig_zeta) - dphi);
+            break;
+        }
+        default:  // change eq. 15 (:196), move eq. 14 (:241)
+            alpha = det_exp(-dphi);
+            break;
+    }
+    if (alpha > 1.0) alpha = 1.0;  // min([1 alpha]...)
+    return p.u_accept < alpha;    // rand(1)[1] < alpha && valid == 1
+}
+
+}  // namespace tdchain

@@ -1,0 +1,64 @@
+// ctx.h -- the td_ctx object behind the C ABI (include/tdstar.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/tdstar.h"
+#include "internal.h"
+
+struct td_ctx {
+    int device = 0;
+    int num_cus = 0;
+    std::string arch;
+    hipStream_t stream = nullptr;
+    tdstar::Geometry g;                 // device-resident ray geometry
+    std::vector<int> ray_off_host;      // CSR offsets (host copy)
+    std::vector<double> hx, hy, hz;     // CSR points (host copy; chain tiles are built from it)
+    std::vector<double> sig_host;
+    double likelihood = 0.0;            // MCsub.jl:179 constant for sig_host
+
+    // one cell set (SoA x|y|z|zeta with stride cell_cap), device + pinned host staging
+    double *cells = nullptr;
+    double *h_cells = nullptr;
+    int64_t cell_cap = 0;
+
+    // per-evaluation outputs / caches
+    tdstar::NNWork nn;
+    int *best_i = nullptr;
+    double *best_d = nullptr;
+    double *zeta0 = nullptr;
+    double *ptS = nullptr;
+    double *phi = nullptr;
+    double *h_out = nullptr;            // pinned: [phi, ptS[n]]
+    int *h_best_i = nullptr;            // pinned [P]
+
+    // query points for td_interpolate
+    double *q = nullptr, *h_q = nullptr;
+    int64_t q_cap = 0;
+    int *q_i = nullptr;
+    double *q_z = nullptr;
+    int *h_q_i = nullptr;
+    double *h_q_z = nullptr;
+
+    tdstar::Timer timer;                // per-kernel HIP-event timing (td_timing_*)
+    std::string err;
+};
+
+namespace tdstar {
+
+// Error helpers shared by api.cpp / chain.cpp.
+int set_err(td_ctx *ctx, int code, const std::string &msg);
+int hip_err(td_ctx *ctx, hipError_t e, const char *what);
+// Make room for `ncells` cells (device + pinned staging).
+int ensure_cells(td_ctx *ctx, int64_t ncells);
+// Pack cells into the pinned staging buffer and upload them (async on ctx->stream).
+int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                 int64_t ncells);
+// Julia Base.sum association (see oracle/README.md); used for the likelihood constant.
+double julia_sum(const double *a, int64_t n);
+double likelihood_constant(const double *sig, int64_t n);
+
+}  // namespace tdstar

@@ -1,0 +1,290 @@
+// kernels.hip -- FP64 forward-model kernels for gfx950 (CDNA4).
+//
+// The three stages of MCsub.jl:123-185 `evaluate`:
+//   1. nearest cell per ray point (v_nearest, MCsub.jl:247-263) -- brute force
+//      over every cell, the only heavy stage (P x N distance evaluations).
+//      Cells are split into chunks staged in LDS (grid.y), points are spread
+//      over lanes (grid.x, PPL points per lane), and the per-chunk partial
+//      minima are merged in chunk order so the FIRST minimum index wins,
+//      exactly as the reference's sequential strict '<' scan.
+//   2. per-ray t* integral (MCsub.jl:147-159) in Julia's Base.sum association
+//      (oracle/README.md: VF=8 x IC=4 accumulators + sequential tail).
+//   3. chi^2 (MCsub.jl:169-172), strictly sequential in k.
+//
+// Numerics: the whole TU is compiled with -ffp-contract=off (and the pragma
+// below) so no a*b+c is fused -- the reference's FP64 rounding is reproduced
+// operation for operation, and nearest indices are bit-exact.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "internal.h"
+#include "ray_sum.h"
+
+namespace tdstar {
+
+namespace {
+
+constexpr int kNNThreads = 256;
+constexpr int kMaxChunk = 2048;  // cells per LDS chunk (64 KiB as double4)
+constexpr int kMinChunk = 64;
+
+// ---------------------------------------------------------------------------
+// Stage 1a: partial nearest over one chunk of cells.
+//   grid.x = point tiles of 256*PPL points, grid.y = cell chunks.
+//   Cells of the chunk are staged as {x,y,z,-} double4 in LDS; every lane
+//   reads the same cell (LDS broadcast, conflict-free) and updates PPL
+//   independent (min distance, first index) pairs.
+// ---------------------------------------------------------------------------
+template <int PPL>
+__global__ __launch_bounds__(kNNThreads) void k_nn_partial(
+    const double *__restrict__ qx, const double *__restrict__ qy, const double *__restrict__ qz,
+    int npts, int ys, int zs, const double *__restrict__ cells, int stride, int ncells, int chunk,
+    double *__restrict__ part_d, int *__restrict__ part_i) {
+    extern __shared__ double4 sc[];
+    const int c0 = blockIdx.y * chunk;
+    const int nc = min(chunk, ncells - c0);
+    for (int j = threadIdx.x; j < nc; j += kNNThreads)
+        sc[j] = make_double4(cells[c0 + j], cells[stride + c0 + j], cells[2 * stride + c0 + j], 0.0);
+
+    double x[PPL], y[PPL], z[PPL], bd[PPL];
+    int bi[PPL];
+    const int base = blockIdx.x * (kNNThreads * PPL) + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        const int p = min(base + k * kNNThreads, npts - 1);
+        x[k] = qx[p];
+        y[k] = qy[(long)p * ys];
+        z[k] = qz[(long)p * zs];
+        bd[k] = kSentinel;
+        bi[k] = -1;
+    }
+    __syncthreads();
+
+#pragma unroll 2
+    for (int j = 0; j < nc; ++j) {
+        const double4 c = sc[j];
+#pragma unroll
+        for (int k = 0; k < PPL; ++k) {
+            // (mx[i]-x)^2 + (my[i]-y)^2 + (mz[i]-z)^2, MCsub.jl:254, left to right, unfused
+            const double dx = c.x - x[k], dy = c.y - y[k], dz = c.z - z[k];
+            double d = dx * dx;
+            d = d + dy * dy;
+            d = d + dz * dz;
+            const bool lt = d < bd[k];  // MCsub.jl:255 strict: NaN never wins
+            bd[k] = lt ? d : bd[k];
+            bi[k] = lt ? c0 + j : bi[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        const int p = base + k * kNNThreads;
+        if (p < npts) {
+            part_d[(long)blockIdx.y * npts + p] = bd[k];
+            part_i[(long)blockIdx.y * npts + p] = bi[k];
+        }
+    }
+}
+
+// Stage 1b: merge the chunk minima in chunk order (strict '<': the lowest
+// chunk, hence the lowest cell index, wins a tie) and gather zeta.
+__global__ __launch_bounds__(256) void k_nn_merge(const double *__restrict__ part_d,
+                                                  const int *__restrict__ part_i, int npts, int chunks,
+                                                  const double *__restrict__ zeta_cells,
+                                                  int *__restrict__ best_i, double *__restrict__ best_d,
+                                                  double *__restrict__ zeta0) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npts) return;
+    double d = kSentinel;
+    int i = -1;
+    for (int c = 0; c < chunks; ++c) {
+        const double dc = part_d[(long)c * npts + p];
+        if (dc < d) {
+            d = dc;
+            i = part_i[(long)c * npts + p];
+        }
+    }
+    if (best_i) best_i[p] = i;
+    if (best_d) best_d[p] = d;
+    if (zeta0) zeta0[p] = (i >= 0) ? zeta_cells[i] : 0.0;  // MCsub.jl:249 v = 0 when nothing < 1e9
+}
+
+// ---------------------------------------------------------------------------
+// Stage 2: per-ray t*.  One 64-lane wave per ray, 4 rays per workgroup
+// (ray_sum.h: Julia's sum association, bit-exact to the oracle).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_ray_sums(const int *__restrict__ ray_off, int n,
+                                                  const double *__restrict__ w,
+                                                  const double *__restrict__ z0, double *__restrict__ ptS) {
+    __shared__ double scratch[4][96];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ray = blockIdx.x * 4 + wv;
+    if (ray >= n) return;  // wave-uniform; no block barrier below
+    const int s0 = ray_off[ray];
+    const int np = ray_off[ray + 1] - s0;
+    const double r = wave_ray_sum(lane, w, PlainZeta{z0}, s0, np, scratch[wv]);
+    if (lane == 0) ptS[ray] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Stage 3: chi^2, MCsub.jl:169-172.  Terms in parallel into LDS, then one
+// lane adds them in k order (the reference's sequential loop, bit for bit).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_chi2(const double *__restrict__ ptS, const double *__restrict__ tS,
+                                              const double *__restrict__ sig, int n, double *__restrict__ phi) {
+    constexpr int kTile = 2048;
+    __shared__ double t[kTile];
+    double C = 0.0;
+    for (int base = 0; base < n; base += kTile) {
+        const int cnt = min(kTile, n - base);
+        for (int k = threadIdx.x; k < cnt; k += 256) {
+            const double d = ptS[base + k] - tS[base + k];
+            const double s = sig[base + k];
+            t[k] = ((d * d) * 1.0) / (s * s);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int k = 0; k < cnt; ++k) C = C + t[k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *phi = C;
+}
+
+}  // namespace
+
+NNPlan plan_nearest(int64_t npts, int64_t ncells, int num_cus) {
+    NNPlan p{};
+    p.ppl = 2;
+    const int64_t per_block = (int64_t)kNNThreads * p.ppl;
+    p.blocks_x = (int)std::max<int64_t>(1, (npts + per_block - 1) / per_block);
+    if (ncells <= 0) {
+        p.chunks = 0;
+        p.chunk = 0;
+        return p;
+    }
+    const int64_t target = (int64_t)std::max(num_cus, 1) * 4;  // ~4 workgroups (16 waves) per CU
+    int64_t chunks = (target + p.blocks_x - 1) / p.blocks_x;
+    chunks = std::min<int64_t>(chunks, (ncells + kMinChunk - 1) / kMinChunk);
+    chunks = std::max<int64_t>(chunks, (ncells + kMaxChunk - 1) / kMaxChunk);
+    chunks = std::max<int64_t>(chunks, 1);
+    p.chunk = (int)((ncells + chunks - 1) / chunks);
+    p.chunks = (int)((ncells + p.chunk - 1) / p.chunk);
+    return p;
+}
+
+hipError_t launch_nearest(const double *qx, const double *qy, const double *qz, int64_t npts,
+                          int64_t qy_stride, int64_t qz_stride, const double *cells, int64_t stride,
+                          int64_t ncells, NNWork &work, int num_cus, int *best_i, double *best_d,
+                          double *zeta0, hipStream_t s, Timer *tm) {
+    if (npts <= 0) return hipSuccess;
+    const NNPlan p = plan_nearest(npts, ncells, num_cus);
+    const size_t need = (size_t)p.chunks * (size_t)npts;
+    if (need > work.cap) {
+        if (work.part_d) (void)hipFree(work.part_d);
+        if (work.part_i) (void)hipFree(work.part_i);
+        work.part_d = nullptr;
+        work.part_i = nullptr;
+        work.cap = 0;
+        hipError_t e = hipMalloc(&work.part_d, need * sizeof(double));
+        if (e != hipSuccess) return e;
+        e = hipMalloc(&work.part_i, need * sizeof(int));
+        if (e != hipSuccess) return e;
+        work.cap = need;
+    }
+    if (p.chunks > 0) {
+        dim3 grid(p.blocks_x, p.chunks);
+        const size_t lds = (size_t)p.chunk * sizeof(double4);
+        hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
+        hipLaunchKernelGGL(k_nn_partial<2>, grid, dim3(kNNThreads), lds, s, qx, qy, qz, (int)npts,
+                           (int)qy_stride, (int)qz_stride, cells, (int)stride, (int)ncells, p.chunk,
+                           work.part_d, work.part_i);
+        if (tm) tm->end("nn_partial", t0, s);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipEvent_t t1 = tm ? tm->begin(s) : nullptr;
+    hipLaunchKernelGGL(k_nn_merge, dim3((unsigned)((npts + 255) / 256)), dim3(256), 0, s, work.part_d,
+                       work.part_i, (int)npts, p.chunks, cells + 3 * stride, best_i, best_d, zeta0);
+    if (tm) tm->end("nn_merge", t1, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm) {
+    if (g.n <= 0) return hipSuccess;
+    hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
+    hipLaunchKernelGGL(k_ray_sums, dim3((unsigned)((g.n + 3) / 4)), dim3(256), 0, s, g.ray_off, (int)g.n, g.w,
+                       zeta0, ptS);
+    if (tm) tm->end("ray_sums", t0, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_chi2(const Geometry &g, const double *ptS, double *phi, hipStream_t s, Timer *tm) {
+    hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
+    hipLaunchKernelGGL(k_chi2, dim3(1), dim3(256), 0, s, ptS, g.tS, g.sig, (int)g.n, phi);
+    if (tm) tm->end("chi2", t0, s);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ Timer ----
+hipEvent_t Timer::begin(hipStream_t s) {
+    if (!on) return nullptr;
+    hipEvent_t e = nullptr;
+    if (!spare.empty()) {
+        e = spare.back();
+        spare.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+        return nullptr;
+    }
+    (void)hipEventRecord(e, s);
+    return e;
+}
+
+void Timer::end(const char *name, hipEvent_t a, hipStream_t s) {
+    if (!on || !a) return;
+    hipEvent_t b = nullptr;
+    if (!spare.empty()) {
+        b = spare.back();
+        spare.pop_back();
+    } else if (hipEventCreate(&b) != hipSuccess) {
+        spare.push_back(a);
+        return;
+    }
+    (void)hipEventRecord(b, s);
+    pending.push_back(Pending{name, a, b});
+}
+
+hipError_t Timer::collect() {
+    for (auto &p : pending) {
+        hipError_t e = hipEventSynchronize(p.b);
+        if (e != hipSuccess) return e;
+        float ms = 0.f;
+        e = hipEventElapsedTime(&ms, p.a, p.b);
+        if (e != hipSuccess) return e;
+        auto &slot = acc[p.name];
+        slot.first += 1;
+        slot.second += ms;
+        spare.push_back(p.a);
+        spare.push_back(p.b);
+    }
+    pending.clear();
+    return hipSuccess;
+}
+
+void Timer::reset() {
+    (void)collect();
+    acc.clear();
+}
+
+void Timer::release() {
+    for (auto &p : pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    pending.clear();
+    for (auto e : spare) (void)hipEventDestroy(e);
+    spare.clear();
+}
+
+}  // namespace tdstar

@@ -1,0 +1,109 @@
+"""Independent numpy restatement of the forward model -- TEST INFRASTRUCTURE ONLY.
+
+Written separately from tstar_oracle.c (vectorised over cells, different code
+path) so the two restatements can check each other where no reference output
+exists (nearest-cell search, ray integral).  Cites the same Julia lines.
+"""
+import math
+
+import numpy as np
+
+
+def nearest_index(px, py, pz, xc, yc, zc):
+    """MCsub.jl:247-263 vectorised: for each point, the first cell index at the
+    minimum FP64 squared distance ((dx^2 + dy^2) + dz^2); -1 when no distance is
+    strictly below the 1e9 sentinel.  NaN distances never win (NaN < m is false)."""
+    px, py, pz = (np.asarray(a, dtype=np.float64).reshape(-1, 1) for a in (px, py, pz))
+    xc, yc, zc = (np.asarray(a, dtype=np.float64).reshape(1, -1) for a in (xc, yc, zc))
+    if xc.shape[1] == 0:
+        return np.full(px.shape[0], -1, dtype=np.int64)
+    dx, dy, dz = xc - px, yc - py, zc - pz
+    d = (dx * dx + dy * dy) + dz * dz  # numpy evaluates left to right, no FMA
+    d = np.where(np.isnan(d), np.inf, d)
+    idx = np.argmin(d, axis=1)  # first occurrence of the minimum
+    best = d[np.arange(d.shape[0]), idx]
+    return np.where(best < 1e9, idx, -1).astype(np.int64)
+
+
+def julia_sum(a, vf=8, ic=4):
+    """Julia 1.5 Base.sum association (see tstar_oracle.c for the derivation)."""
+    a = [float(v) for v in a]
+    n = len(a)
+    if n == 0:
+        return 0.0
+    if n == 1:
+        return a[0]
+    if n < 16:
+        s = a[0] + a[1]
+        for v in a[2:]:
+            s = s + v
+        return s
+
+    def block(f, l):
+        if f == l:
+            return a[f]
+        v = a[f] + a[f + 1]
+        T = l - f - 1
+        W = vf * ic
+        Q = T // W if T >= W else 0
+        i = f + 2
+        if Q:
+            acc = np.zeros((ic, vf))
+            acc[0, 0] = v
+            blk = np.asarray(a[i:i + Q * W]).reshape(Q, ic, vf)
+            for q in range(Q):
+                acc = acc + blk[q]
+            r = acc[0].copy()
+            for k in range(1, ic):
+                r = acc[k] + r
+            h = vf // 2
+            while h >= 1:
+                r = r[:h] + r[h:2 * h]
+                h //= 2
+            v = float(r[0])
+            i += Q * W
+        for j in range(i, l + 1):
+            v = v + a[j]
+        return v
+
+    def impl(f, l):
+        if l - f < 1024:
+            return block(f, l)
+        mid = f + ((l - f) >> 1)
+        return impl(f, mid) + impl(mid + 1, l)
+
+    return impl(0, n - 1)
+
+
+def chi2(ptS, tS, allSig):
+    """MCsub.jl:169-172 (sequential in k)."""
+    C = 0.0
+    for p, t, s in zip(ptS, tS, allSig):
+        d = float(p) - float(t)
+        C = C + ((d * d) * 1.0) / (float(s) * float(s))
+    return C
+
+
+def likelihood(allSig):
+    """MCsub.jl:179."""
+    n = len(allSig)
+    c = math.sqrt(2 * math.pi)
+    return julia_sum([(-math.log(float(s) * c)) * float(n) for s in allSig])
+
+
+def evaluate_csr(npts, px, py, pz, w, tS, allSig, cells):
+    """MCsub.jl:123-185 on the compact layout: npts[i] valid points of ray i
+    stored consecutively; w[k] = rayL*rayU of the segment starting at point k
+    (ignored for the last point of each ray).  Returns (ptS, phi, lik, nearest)."""
+    xc, yc, zc, ze = (np.asarray(a, dtype=np.float64) for a in cells)
+    idx = nearest_index(px, py, pz, xc, yc, zc)
+    zeta0 = np.where(idx >= 0, ze[np.maximum(idx, 0)] if len(ze) else 0.0, 0.0)
+    ptS = np.zeros(len(npts))
+    off = 0
+    for i, c in enumerate(npts):
+        z = zeta0[off:off + c]
+        rz = 0.5 * (z[:-1] + z[1:])
+        terms = w[off:off + c - 1] * (rz / 1000.0) if c > 1 else np.zeros(0)
+        ptS[i] = julia_sum(terms)
+        off += c
+    return ptS, chi2(ptS, tS, allSig), likelihood(allSig), idx

@@ -1,0 +1,99 @@
+"""GPU parity of the rj-MCMC chain (TD_inversion_function.jl:70-274).
+
+The DEVICE engine (one persistent workgroup, incremental forward model) must
+follow the HOST engine -- which evaluates every proposal with a full
+td_evaluate exactly as the reference does -- bit for bit: same accepted
+proposals, same phi after every run, same final model.  And the cached chain
+state must equal a from-scratch evaluate of its model at any time."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(tt, ds):
+    return tt.TdContext.from_datastruct(ds)
+
+
+def make(tt, ctx, prm, model, seed, engine, T=1.0, chain=1):
+    p = tt.chain_params(prm, None, seed=seed, chain=chain, temperature=T, engine=engine)
+    return tt.Chain(ctx, p, model)
+
+
+def same_models(a, b):
+    return (len(a.xCell) == len(b.xCell) and np.array_equal(a.xCell, b.xCell) and np.array_equal(a.yCell, b.yCell)
+            and np.array_equal(a.zCell, b.zCell) and np.array_equal(a.zeta, b.zeta))
+
+
+@pytest.mark.parametrize("ncells,max_cells,iters,seed", [(200, 300, 400, 1), (1000, 1100, 250, 2),
+                                                         (5000, 5100, 120, 3), (8, 12, 600, 4)])
+def test_device_engine_follows_host_engine(tt, ds, ctx, ncells, max_cells, iters, seed):
+    prm = tt.define_TDstructrure().replace(max_cells=max_cells)
+    model = tt.random_model(ncells, seed)
+    dev = make(tt, ctx, prm, model, seed, tt.TD_ENGINE_DEVICE)
+    host = make(tt, ctx, prm, model, seed, tt.TD_ENGINE_HOST)
+    for _ in range(4):
+        dev.run(iters // 4)
+        host.run(iters // 4)
+        sd, sh = dev.stats(), host.stats()
+        assert sd["phi"] == sh["phi"], (sd, sh)
+        assert sd["accepted"] == sh["accepted"] and sd["proposed"] == sh["proposed"]
+        assert sd["ncells"] == sh["ncells"]
+    assert same_models(dev.model(), host.model())
+    assert sum(sd["accepted"]) > 0
+
+
+def test_chain_state_equals_full_evaluate(tt, ds, ctx):
+    prm = tt.define_TDstructrure().replace(max_cells=2200)
+    dev = make(tt, ctx, prm, tt.random_model(2000, 100), 100, tt.TD_ENGINE_DEVICE)
+    for _ in range(5):
+        dev.run(300)
+        m = dev.model()
+        ptS, phi, _, _ = ctx.evaluate(m.cells())
+        assert phi == m.phi == dev.stats()["phi"]
+        assert np.array_equal(ptS, m.ptS)
+
+
+def test_tempered_chain_matches_host(tt, ds, ctx):
+    prm = tt.define_TDstructrure().replace(max_cells=400)
+    model = tt.random_model(300, 9)
+    dev = make(tt, ctx, prm, model, 9, tt.TD_ENGINE_DEVICE, T=4.0, chain=3)
+    host = make(tt, ctx, prm, model, 9, tt.TD_ENGINE_HOST, T=4.0, chain=3)
+    dev.run(300)
+    host.run(300)
+    assert dev.stats()["phi"] == host.stats()["phi"]
+    dev.set_temperature(1.5)
+    host.set_temperature(1.5)
+    dev.run(200)
+    host.run(200)
+    assert dev.stats()["phi"] == host.stats()["phi"]
+    assert same_models(dev.model(), host.model())
+
+
+def test_debug_prior_samples_prior(tt, ds, ctx):
+    prm = tt.define_TDstructrure().replace(debug_prior=1)
+    dev = make(tt, ctx, prm, None, 21, tt.TD_ENGINE_DEVICE)
+    host = make(tt, ctx, prm, None, 21, tt.TD_ENGINE_HOST)
+    counts = []
+    for _ in range(20):
+        dev.run(500)
+        host.run(500)
+        m = dev.model()
+        counts.append(len(m.xCell))
+        assert same_models(m, host.model())
+        assert 5 <= len(m.xCell) <= 100
+        assert np.all((m.zeta > 0) & (m.zeta < 50))
+        assert dev.stats()["phi"] == 1.0
+    assert len(set(counts)) > 3  # the dimension actually moves
+
+
+def test_reference_driver_thinning(tt, ds):
+    prm = tt.define_TDstructrure().replace(n_iter=300.0, burn_in=100.0, keep_each=20.0, print_each=100.0,
+                                           max_cells=200)
+    hist = tt.TD_inversion_function(prm, ds, 1, seed=5)
+    assert len(hist) == 10  # (n_iter - burn_in) / keep_each
+    for m in hist[::3]:
+        m2 = m.copy()
+        tt.evaluate(m2, ds, prm)
+        assert m2.phi == m.phi
