@@ -28,6 +28,11 @@ void tdt_draws(uint64_t seed, uint32_t chain, uint64_t iter, double out[7]);
  * Interpolation value at the birth site (needed to draw zetanew). */
 int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const double *cx, const double *cy,
                 const double *cz, const double *czeta, double czeta_birth, double out[8]);
+/* Diagnostic: turn the DEVICE engine's per-phase s_memtime stamps on/off and
+ * read the accumulated shader cycles per phase (0 draw, 1 birth/death query,
+ * 2 tiles, 3 points, 4 orphans, 5 ray marks, 6 ray sums, 7 chi^2, 8 accept,
+ * 9 commit).  Never enabled in measured runs. */
+int tdt_chain_profile(td_chain *ch, int enable, int64_t out[16]);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);

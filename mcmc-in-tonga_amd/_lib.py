@@ -73,6 +73,7 @@ SIGNATURES = {
     "tdt_normal_quantile": (_d, [_d]),
     "tdt_draws": (None, [_u64, _u32, _u64, _pd]),
     "tdt_propose": (ctypes.c_int, [ctypes.POINTER(TdChainParams), _u64, _i64, _pd, _pd, _pd, _pd, _d, _pd]),
+    "tdt_chain_profile": (ctypes.c_int, [_vp, ctypes.c_int, _pi64]),
     "tdt_accept": (ctypes.c_int, [ctypes.POINTER(TdChainParams), ctypes.c_int, _d, _d, _i64, _d, _d, _d, _d, _d]),
 }
 

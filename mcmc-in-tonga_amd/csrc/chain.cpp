@@ -36,6 +36,7 @@ struct td_chain {
     td_chain_stats stats{};
     // device engine
     DevChain dev{};
+    DevChain *dev_ptr = nullptr;  // device copy the kernel reads
     void *dev_block = nullptr;  // one allocation for every device array
     ChainScalars *st_dev = nullptr;
     ChainScalars *st_host = nullptr;  // pinned
@@ -165,7 +166,8 @@ T *carve(char *&cur, size_t count) {
 int device_setup(td_chain *ch) {
     td_ctx *c = ch->ctx;
     const int64_t P = c->g.P, n = c->g.n;
-    // ---- tiles: <= kTilePts consecutive points of one ray, FP64 bounding boxes ----
+    // ---- tiles: <= kTilePts consecutive points of one ray; bounding boxes
+    //      rounded OUTWARD to FP32 (the lower bound stays valid, LDS holds them) ----
     std::vector<int> tstart, tile_of((size_t)P), pt_ray((size_t)P);
     for (int64_t r = 0; r < n; ++r) {
         const int a = c->ray_off_host[(size_t)r], b = c->ray_off_host[(size_t)r + 1];
@@ -174,7 +176,7 @@ int device_setup(td_chain *ch) {
     }
     const int ntiles = (int)tstart.size();
     tstart.push_back((int)P);
-    std::vector<double> lo(3 * (size_t)ntiles), hi(3 * (size_t)ntiles);
+    std::vector<float> lo(3 * (size_t)ntiles), hi(3 * (size_t)ntiles);
     for (int t = 0; t < ntiles; ++t) {
         double l[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, h[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
         for (int q = tstart[(size_t)t]; q < tstart[(size_t)t + 1]; ++q) {
@@ -187,24 +189,53 @@ int device_setup(td_chain *ch) {
                 }
         }
         for (int a = 0; a < 3; ++a) {
-            lo[(size_t)a * ntiles + t] = l[a];
-            hi[(size_t)a * ntiles + t] = h[a];
+            float fl = (float)l[a], fh = (float)h[a];
+            if ((double)fl > l[a]) fl = std::nextafter(fl, -HUGE_VALF);
+            if ((double)fh < h[a]) fh = std::nextafter(fh, HUGE_VALF);
+            lo[(size_t)a * ntiles + t] = fl;
+            hi[(size_t)a * ntiles + t] = fh;
         }
     }
     ch->tile_start_host = tstart;
     const int cap = std::max<int>(ch->prm.max_cells, (int)ch->x.size()) + 1;
+    // ---- bucket grid over the cells: ~2 cells per bucket at the starting size ----
+    CellGrid G{};
+    {
+        const double ex = ch->P.xmax - ch->P.xmin, ey = ch->P.ymax - ch->P.ymin, ez = ch->P.zmax - ch->P.zmin;
+        const double vol = std::max(ex, 1e-6) * std::max(ey, 1e-6) * std::max(ez, 1e-6);
+        const double nref = std::max<double>((double)ch->x.size(), 16.0);
+        const double h = std::cbrt(vol / std::max(1.0, nref / 2.0));
+        auto dim = [&](double e) { return e > 0.0 ? (int)std::min(256.0, std::max(1.0, std::ceil(e / h))) : 1; };
+        G.gx = dim(ex); G.gy = dim(ey); G.gz = dim(ez);
+        G.x0 = ch->P.xmin; G.y0 = ch->P.ymin; G.z0 = ch->P.zmin;
+        G.ix = ex > 0.0 ? G.gx / ex : 0.0; G.iy = ey > 0.0 ? G.gy / ey : 0.0; G.iz = ez > 0.0 ? G.gz / ez : 0.0;
+        G.hx = ex > 0.0 ? ex / G.gx : 0.0; G.hy = ey > 0.0 ? ey / G.gy : 0.0; G.hz = ez > 0.0 ? ez / G.gz : 0.0;
+    }
+    const size_t nbuckets = (size_t)G.gx * G.gy * G.gz;
+    std::vector<int> bcount(nbuckets, 0);
+    std::vector<BucketEntry> bent(nbuckets * kBucketCap, BucketEntry{0.0, 0.0, 0.0, 0, 0});
+    int overflow = 0;
+    for (size_t i = 0; i < ch->x.size(); ++i) {
+        const int b = grid_bucket(G, ch->x[i], ch->y[i], ch->z[i]);
+        if (bcount[(size_t)b] < kBucketCap)
+            bent[(size_t)b * kBucketCap + bcount[(size_t)b]++] = BucketEntry{ch->x[i], ch->y[i], ch->z[i], (int)i, 0};
+        else
+            overflow = 1;
+    }
     // ---- one device block for everything the chain owns ----
     size_t bytes = 0;
     auto add = [&](size_t b) { bytes += ((b + 255) / 256) * 256; };
     const size_t Pn = (size_t)std::max<int64_t>(P, 1), nn = (size_t)std::max<int64_t>(n, 1);
     add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * Pn); add(sizeof(int) * Pn);
-    add(sizeof(double) * 3 * ntiles); add(sizeof(double) * 3 * ntiles); add(sizeof(double) * (ntiles + 1));
+    add(sizeof(float) * 3 * ntiles); add(sizeof(float) * 3 * ntiles); add(sizeof(double) * (ntiles + 1));
     add(sizeof(double) * 4 * cap); for (int i = 0; i < 4; ++i) add(sizeof(int) * cap);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn); add(Pn);
     add(sizeof(int) * Pn); add(sizeof(int) * Pn); add(sizeof(int) * (ntiles + 1));
     for (int i = 0; i < 4; ++i) add(sizeof(double) * nn);
     add(sizeof(int) * nn); add(sizeof(int) * nn); add(sizeof(ChainScalars));
+    add(sizeof(int) * nbuckets); add(sizeof(BucketEntry) * nbuckets * kBucketCap); add(sizeof(int));
+    add(sizeof(DevChain));
     hipError_t e = hipMalloc(&ch->dev_block, bytes);
     if (e != hipSuccess) return hip_err(c, e, "hipMalloc(chain state)");
     e = hipMemsetAsync(ch->dev_block, 0, bytes, c->stream);
@@ -218,9 +249,9 @@ int device_setup(td_chain *ch) {
     int *tile_start = carve<int>(cur, ntiles + 1);
     int *tile_of_d = carve<int>(cur, Pn);
     int *pt_ray_d = carve<int>(cur, Pn);
-    double *tlo = carve<double>(cur, 3 * (size_t)ntiles);
-    double *thi = carve<double>(cur, 3 * (size_t)ntiles);
-    d.tile_start = tile_start; d.tile_of = tile_of_d; d.pt_ray = pt_ray_d; d.tile_lo = tlo; d.tile_hi = thi;
+    float *tlo = carve<float>(cur, 3 * (size_t)ntiles);
+    float *thi = carve<float>(cur, 3 * (size_t)ntiles);
+    d.tile_start = tile_start; d.pt_ray = pt_ray_d; d.tile_lo = tlo; d.tile_hi = thi;
     d.tile_maxd = carve<double>(cur, ntiles + 1);
     d.ntiles = ntiles;
     double *cells = carve<double>(cur, 4 * (size_t)cap);
@@ -236,6 +267,11 @@ int device_setup(td_chain *ch) {
     d.prefix = carve<double>(cur, nn); d.cand_prefix = carve<double>(cur, nn);
     d.rays_hit = carve<int>(cur, nn); d.ray_flag = carve<int>(cur, nn);
     d.st = carve<ChainScalars>(cur, 1);
+    d.grid = G;
+    d.bucket_count = carve<int>(cur, nbuckets);
+    d.buckets = carve<BucketEntry>(cur, nbuckets * kBucketCap);
+    d.grid_overflow = carve<int>(cur, 1);
+    ch->dev_ptr = carve<DevChain>(cur, 1);
     ch->st_dev = d.st;
     d.params = ch->P;
     d.seed = ch->prm.seed;
@@ -245,8 +281,9 @@ int device_setup(td_chain *ch) {
     if (e != hipSuccess) return hip_err(c, e, "hipHostMalloc(chain scalars)");
     // ---- uploads ----
     const int N = (int)ch->x.size();
-    std::vector<int> ident((size_t)cap);
+    std::vector<int> ident((size_t)cap), rank0((size_t)cap, -1);  // slots >= N are free
     for (int i = 0; i < cap; ++i) ident[(size_t)i] = i;
+    for (int i = 0; i < N; ++i) rank0[(size_t)i] = i;
     std::vector<double> hc(4 * (size_t)cap, 0.0);
     std::copy(ch->x.begin(), ch->x.end(), hc.begin());
     std::copy(ch->y.begin(), ch->y.end(), hc.begin() + cap);
@@ -262,11 +299,14 @@ int device_setup(td_chain *ch) {
         {tile_start, tstart.data(), sizeof(int) * tstart.size()},
         {tile_of_d, tile_of.data(), sizeof(int) * (size_t)P},
         {pt_ray_d, pt_ray.data(), sizeof(int) * (size_t)P},
-        {tlo, lo.data(), sizeof(double) * lo.size()},
-        {thi, hi.data(), sizeof(double) * hi.size()},
+        {tlo, lo.data(), sizeof(float) * lo.size()},
+        {thi, hi.data(), sizeof(float) * hi.size()},
         {cells, hc.data(), sizeof(double) * hc.size()},
         {d.order, ident.data(), sizeof(int) * (size_t)cap},
-        {d.rank, ident.data(), sizeof(int) * (size_t)cap},
+        {d.rank, rank0.data(), sizeof(int) * (size_t)cap},
+        {d.bucket_count, bcount.data(), sizeof(int) * nbuckets},
+        {d.buckets, bent.data(), sizeof(BucketEntry) * bent.size()},
+        {d.grid_overflow, &overflow, sizeof(int)},
         {d.st, &s0, sizeof s0}};
     for (auto &u : ups)
         if (u.b) {
@@ -391,7 +431,9 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
     }
     Timer *tm = ch->ctx->timer.on ? &ch->ctx->timer : nullptr;
     hipEvent_t t0 = tm ? tm->begin(ch->ctx->stream) : nullptr;
-    e = chain_run(ch->dev, iterations, ch->ctx->stream);
+    e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, ch->ctx->stream);
+    if (e != hipSuccess) return hip_err(ch->ctx, e, "chain descriptor upload");
+    e = chain_run(ch->dev, ch->dev_ptr, iterations, ch->ctx->stream);
     if (tm) tm->end("chain_run", t0, ch->ctx->stream);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "k_chain_run launch");
     const int64_t before = ch->stats.iterations;
@@ -479,6 +521,17 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
     const double v[8] = {(double)p.action, (double)p.active, (double)p.valid, (double)p.index, p.x, p.y, p.z, p.zeta};
     std::memcpy(out, v, sizeof v);
     return 0;
+}
+int tdt_chain_profile(td_chain *ch, int enable, int64_t out[16]) {
+    if (!ch || ch->engine != TD_ENGINE_DEVICE) return TD_ERR_ARG;
+    ch->dev.profile = enable;
+    if (out) {
+        ChainScalars s{};
+        hipError_t e = hipMemcpy(&s, ch->st_dev, sizeof s, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_err(ch->ctx, e, "tdt_chain_profile");
+        std::memcpy(out, s.prof, sizeof s.prof);
+    }
+    return TD_OK;
 }
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death) {

@@ -6,12 +6,15 @@
 // (slot, squared distance, zeta) of its nearest cell -- exactly what a full
 // v_nearest scan would give -- so a proposal only touches:
 //   birth : points the new cell captures (d < cached d)
-//   death : points whose cell is the killed one (full re-search of those)
+//   death : points whose cell is the killed one (re-searched)
 //   change: points whose cell is the changed one (zeta only)
-//   move  : points of the moved cell (re-search) + points it captures
-// Candidate points are found through 16-point ray tiles whose FP64 bounding
-// boxes give an exact lower bound of the distance (computed with the same
-// rounded operations as the distance itself, so LB <= d holds bit-wise).
+//   move  : points of the moved cell (re-searched) + points it captures
+// Candidate points are found through 16-point ray tiles whose bounding boxes
+// give an exact lower bound of the distance (monotone rounding: lb <= d
+// bit-wise).  Re-searches and the birth/death Interpolation queries go
+// through a uniform bucket grid over the cells, proven by a lower bound on
+// everything outside the 3x3x3 block searched; otherwise (or on an exact
+// distance tie, or a full bucket) they scan every slot.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -23,7 +26,8 @@
 namespace tdstar {
 
 constexpr int kTilePts = 16;
-constexpr int kChainThreads = 1024;
+constexpr int kChainThreads = 512;  // 8 waves: 256 VGPRs per lane, no spills
+constexpr int kBucketCap = 32;
 
 struct ChainScalars {
     int64_t iter;          // next iteration index
@@ -32,11 +36,37 @@ struct ChainScalars {
     int64_t proposed[5];
     double phi;
     int64_t bytes;         // algorithmic global-memory bytes the proposals needed (roofline)
+    int64_t prof[16];      // diagnostic: shader cycles per phase (DevChain::profile); [15] grid fallbacks
     int ncells;            // cells in the model
     int nslots;            // slot high-water mark
     int nfree;             // free-slot stack depth
     int pad;
 };
+
+// Bucket of a coordinate: clamp(floor((v - v0) * inv), 0, g - 1).  Cells
+// outside the box land in the boundary buckets, so "no bucket beyond" really
+// means no cell beyond.  Same function on host (build) and device (updates).
+struct CellGrid {
+    int gx, gy, gz;
+    double x0, y0, z0;
+    double ix, iy, iz;  // buckets per km
+    double hx, hy, hz;  // km per bucket
+};
+
+struct BucketEntry {
+    double x, y, z;
+    int slot, pad;
+};
+
+__host__ __device__ inline int grid_axis(double v, double v0, double inv, int g) {
+    const double f = (v - v0) * inv;
+    return f >= 0.0 ? (f < (double)g ? (int)f : g - 1) : 0;  // NaN -> 0
+}
+
+__host__ __device__ inline int grid_bucket(const CellGrid &G, double x, double y, double z) {
+    return (grid_axis(z, G.z0, G.iz, G.gz) * G.gy + grid_axis(y, G.y0, G.iy, G.gy)) * G.gx +
+           grid_axis(x, G.x0, G.ix, G.gx);
+}
 
 struct DevChain {
     // geometry (owned by the td_ctx)
@@ -44,10 +74,9 @@ struct DevChain {
     const int *ray_off, *pt_ray;
     int P, n;
     // tiles of <= kTilePts consecutive points of one ray
-    const int *tile_start;  // [ntiles+1]
-    const int *tile_of;     // [P]
-    const double *tile_lo, *tile_hi;  // [3][ntiles] SoA
-    double *tile_maxd;      // [ntiles] max cached distance of the tile's points
+    const int *tile_start;            // [ntiles+1]
+    const float *tile_lo, *tile_hi;   // [3][ntiles] SoA, outward-rounded to FP32
+    double *tile_maxd;                // [ntiles] max cached distance of the tile's points
     int ntiles;
     // cells by slot
     double *cx, *cy, *cz, *czeta;  // [cap]
@@ -68,12 +97,19 @@ struct DevChain {
     tdchain::Params params;
     uint64_t seed;
     uint32_t chain;
+    int profile;  // diagnostic phase stamps (s_memtime) -- off in measured runs
+    // uniform bucket grid over the cells
+    CellGrid grid;
+    int *bucket_count;      // [G]
+    BucketEntry *buckets;   // [G * kBucketCap]
+    int *grid_overflow;     // sticky: a bucket overflowed -> always scan all cells
 };
 
 // Build the cache from scratch for the cells currently in slots 0..ncells-1
 // (order = rank = identity): nearest search, ray sums, chi^2 prefix, tile maxima.
 hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, hipStream_t s);
 // Run `iters` iterations inside one persistent workgroup.
-hipError_t chain_run(const DevChain &d, int64_t iters, hipStream_t s);
+// `dptr` = device copy of `d` (the kernel reads its fields from global memory).
+hipError_t chain_run(const DevChain &d, const DevChain *dptr, int64_t iters, hipStream_t s);
 
 }  // namespace tdstar

@@ -5,15 +5,25 @@
 // proposal (chain_logic.h, shared with the host engine), evaluate it
 // incrementally against the cached per-point nearest cells (chain_dev.h),
 // recompute t* only for the rays whose points changed (Julia sum order,
-// ray_sum.h) and chi^2 only from the first changed ray on (the cached
-// prefix sums ARE the reference's sequential partial sums), then accept or
-// reject.  Every phi it produces is bit-identical to a full evaluate of the
-// proposed model (tests/test_gpu_chain.py checks it against the host engine).
+// ray_sum.h) and chi^2 only from the first changed ray on (the cached prefix
+// sums ARE the reference's sequential partial sums), then accept or reject.
+// Every phi it produces is bit-identical to a full evaluate of the proposed
+// model (tests/test_gpu_chain.py checks it against the host engine).
 //
 // Why one workgroup: a proposal touches ~P/N points and a few rays, i.e.
-// microseconds of work; a grid-wide barrier costs 4-10 us on MI355X
-// (MI355X_MICROARCH.md, barrier-xcd), a kernel boundary ~1.5 us.  One CU keeps
-// the loop free of both; the ~1 MB of geometry + cache stays in its XCD's L2.
+// microseconds of latency-bound work; a grid-wide barrier costs 4-10 us on
+// MI355X (MI355X_MICROARCH.md, barrier-xcd) and a kernel boundary ~1.5 us.
+// One CU keeps the loop free of both.  What bounds an iteration is then the
+// chain of dependent memory round trips and barriers, so:
+//   * tile boxes (FP32, outward-rounded), tile maxima, every per-ray array and
+//     the position->slot map live in LDS when they fit (SMALL: the 381-ray
+//     configs) and are written back to HBM when the launch ends;
+//   * the RNG draws of 64 iterations are computed ahead, one lane each;
+//   * nearest-cell queries go through the bucket grid, one wave per query,
+//     one round of loads, and overlap the tile pass;
+//   * candidate flags are cleared, and the bucket grid updated, at the start of
+//     the NEXT iteration, off the critical path;
+//   * the sequential chi^2 tail runs on one lane from LDS, 8 terms per trip.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -30,6 +40,10 @@ namespace {
 
 using tdchain::Proposal;
 
+constexpr int kWaves = kChainThreads / 64;
+constexpr int kBatch = kWaves;  // query points searched together (one wave each)
+constexpr int kSub = 4;         // queries per full-scan pass (register budget)
+
 __device__ __forceinline__ double dist2(double cx, double cy, double cz, double x, double y, double z) {
     // (mx-x)^2 + (my-y)^2 + (mz-z)^2, MCsub.jl:254 -- same ops as k_nn_partial
     const double dx = cx - x, dy = cy - y, dz = cz - z;
@@ -39,18 +53,22 @@ __device__ __forceinline__ double dist2(double cx, double cy, double cz, double 
     return d;
 }
 
-// Lower bound of dist2(q, p) over every point p of a tile, computed with the
-// same rounded operations (rounding is monotone, so lb2 <= dist2 bit-wise).
-__device__ __forceinline__ double tile_lb2(const DevChain &d, int t, double qx, double qy, double qz) {
-    const int nt = d.ntiles;
-    auto gap = [](double q, double lo, double hi) { return q < lo ? lo - q : (q > hi ? q - hi : 0.0); };
-    const double gx = gap(qx, d.tile_lo[t], d.tile_hi[t]);
-    const double gy = gap(qy, d.tile_lo[nt + t], d.tile_hi[nt + t]);
-    const double gz = gap(qz, d.tile_lo[2 * nt + t], d.tile_hi[2 * nt + t]);
-    double s = gx * gx;
-    s = s + gy * gy;
-    s = s + gz * gz;
-    return s;
+// (distance, Julia position) lexicographic order; a cell must also beat the
+// 1e9 sentinel strictly (MCsub.jl:250,255).
+__device__ __forceinline__ bool better(double d, int r, double bd, int br) {
+    return d < bd || (d == bd && d < kSentinel && r < br);
+}
+
+__device__ __forceinline__ void wave_min_dr(double &dd, int &rr) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double od = __shfl_xor(dd, off, 64);
+        const int orr = __shfl_xor(rr, off, 64);
+        if (better(od, orr, dd, rr)) {
+            dd = od;
+            rr = orr;
+        }
+    }
 }
 
 struct OverlayZeta {
@@ -59,294 +77,626 @@ struct OverlayZeta {
     __device__ __forceinline__ double operator()(int k) const { return flag[k] ? cand[k] : cur[k]; }
 };
 
-// lexicographic (distance, position) minimum across a wave
-__device__ __forceinline__ void wave_min_dj(double &dd, int &jj) {
+struct Shared {
+    Proposal p;
+    double czeta, zeta_killed, zetanew_death, kx, ky, kz, phi_n;
+    int slot_k, new_slot, accept, eval;
+    int n_tiles, n_changed, n_orphans, n_rays, k0;
+    int clr_changed, clr_rays;  // flags to clear at the start of the next iteration
+    int pts_seen, ray_pts;
+    // pending bucket-grid update (applied by the last wave next iteration)
+    int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site
+    double g_ox, g_oy, g_oz, g_nx, g_ny, g_nz;
+    // chain scalars, resident for the whole launch
+    long long iter, evaluations, bytes, grid_fallbacks;
+    long long proposed[5], accepted[5];
+    double phi;
+    int ncells, nslots, nfree;
+    // nearest-cell queries
+    double qx[kBatch], qy[kBatch], qz[kBatch];
+    double res_d[kBatch], res_z[kBatch];
+    int res_s[kBatch];
+    int any_full;
+    double red_d[kWaves][kSub];
+    int red_r[kWaves][kSub];
+    long long prof[16], t_last;  // diagnostic phase stamps
+};
+
+// Diagnostic phase stamp (lane 0 of wave 0, right after a barrier): cycles
+// since the previous stamp are charged to phase k.  Off unless d.profile.
+#define STAMP(k)                                   \
+    do {                                           \
+        if (prof_on && tid == 0) {                 \
+            const long long t_ = clock64();        \
+            sh.prof[k] += t_ - sh.t_last;          \
+            sh.t_last = t_;                        \
+        }                                          \
+    } while (0)
+
+// LDS carve-up (host and device agree on it through this function).
+struct LdsPlan {
+    size_t scratch, chi, draws, tlo, thi, tmaxd, tstart, thit, rayoff, ptS, prefix, cptS, cprefix, tS, sig, rflag,
+        rhit, ord, total;
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool small) {
+    LdsPlan L{};
+    size_t o = align16(sizeof(Shared));
+    L.scratch = o; o += align16(sizeof(double) * kWaves * 96);
+    L.chi = o; o += align16(sizeof(double) * (small ? (n > 0 ? n : 1) : 2048));  // chi^2 terms
+    L.draws = o; o += align16(sizeof(tdchain::Draws) * 64);                     // 64 iterations ahead
+    if (small) {
+        L.tlo = o; o += align16(sizeof(float) * 3 * ntiles);
+        L.thi = o; o += align16(sizeof(float) * 3 * ntiles);
+        L.tmaxd = o; o += align16(sizeof(double) * ntiles);
+        L.tstart = o; o += align16(sizeof(int) * (ntiles + 1));
+        L.thit = o; o += align16(sizeof(int) * (ntiles + 1));
+        L.rayoff = o; o += align16(sizeof(int) * (n + 1));
+        L.ptS = o; o += align16(sizeof(double) * n);
+        L.prefix = o; o += align16(sizeof(double) * n);
+        L.cptS = o; o += align16(sizeof(double) * n);
+        L.cprefix = o; o += align16(sizeof(double) * n);
+        L.tS = o; o += align16(sizeof(double) * n);
+        L.sig = o; o += align16(sizeof(double) * n);
+        L.rflag = o; o += align16(sizeof(int) * n);
+        L.rhit = o; o += align16(sizeof(int) * n);
+        L.ord = o; o += align16(sizeof(int) * cap);
+    }
+    L.total = o;
+    return L;
+}
+
+// Views of the arrays a launch works on: LDS copies in SMALL mode, else HBM.
+struct Views {
+    const float *tlo, *thi;
+    double *tmaxd, *ptS, *prefix, *cptS, *cprefix, *chi;
+    const double *tS, *sig;
+    const int *tstart, *ray_off;
+    int *thit, *rflag, *rhit, *ord;
+};
+
+// Exact nearest live cell by scanning every slot (lexicographic distance,
+// Julia position), kSub queries per pass.  Fallback of the grid search
+// (rare: kept out of line so it does not cost the hot loop registers).
+__device__ __attribute__((noinline)) void block_search(const DevChain &d, const Views &v, Shared &sh, int nq, int skip, int moved, double mx,
+                             double my, double mz) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nslots = sh.nslots;
+    for (int q0 = 0; q0 < nq; q0 += kSub) {
+        double bd[kSub];
+        int br[kSub];
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double od = __shfl_xor(dd, off, 64);
-        const int oj = __shfl_xor(jj, off, 64);
-        if (od < dd || (od == dd && oj < jj)) {
-            dd = od;
-            jj = oj;
+        for (int q = 0; q < kSub; ++q) {
+            bd[q] = kSentinel;
+            br[q] = INT_MAX;
+        }
+        constexpr int kScanUnroll = 8;  // all loads of a round issued before any use
+        for (int s0 = tid; s0 < nslots; s0 += kScanUnroll * kChainThreads) {
+            int r[kScanUnroll];
+            double x[kScanUnroll], y[kScanUnroll], z[kScanUnroll];
+#pragma unroll
+            for (int u = 0; u < kScanUnroll; ++u) {
+                // unconditional loads from a clamped slot, masked afterwards (a select
+                // on the LOAD would make hipcc branch and wait per element)
+                const int s = min(s0 + u * kChainThreads, d.cap - 1);
+                r[u] = d.rank[s];
+                x[u] = d.cx[s];
+                y[u] = d.cy[s];
+                z[u] = d.cz[s];
+            }
+#pragma unroll
+            for (int u = 0; u < kScanUnroll; ++u) {
+                const int s = s0 + u * kChainThreads;
+                if (s >= nslots || r[u] < 0 || s == skip) continue;  // free slot / killed cell
+                if (s == moved) {
+                    x[u] = mx;
+                    y[u] = my;
+                    z[u] = mz;
+                }
+#pragma unroll
+                for (int q = 0; q < kSub; ++q)
+                    if (q0 + q < nq) {
+                        const double dd = dist2(x[u], y[u], z[u], sh.qx[q0 + q], sh.qy[q0 + q], sh.qz[q0 + q]);
+                        if (better(dd, r[u], bd[q], br[q])) {
+                            bd[q] = dd;
+                            br[q] = r[u];
+                        }
+                    }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kSub; ++q)
+            if (q0 + q < nq) {
+                wave_min_dr(bd[q], br[q]);
+                if (lane == 0) {
+                    sh.red_d[wv][q] = bd[q];
+                    sh.red_r[wv][q] = br[q];
+                }
+            }
+        __syncthreads();
+        if (tid < kSub && q0 + tid < nq) {
+            double b = sh.red_d[0][tid];
+            int r = sh.red_r[0][tid];
+            for (int w = 1; w < kWaves; ++w)
+                if (better(sh.red_d[w][tid], sh.red_r[w][tid], b, r)) {
+                    b = sh.red_d[w][tid];
+                    r = sh.red_r[w][tid];
+                }
+            const int s = r != INT_MAX ? v.ord[r] : -1;
+            sh.res_d[q0 + tid] = b;
+            sh.res_s[q0 + tid] = s;
+            sh.res_z[q0 + tid] = s >= 0 ? d.czeta[s] : 0.0;
+        }
+        __syncthreads();
+    }
+}
+
+// Nearest live cell through the bucket grid: wave q handles query q.  Lanes
+// 0..53 cover the 3x3x3 buckets around the query, 8 entries per bucket
+// (entries hold the cell coordinates inline: ONE round of loads).  The answer
+// is proven when its distance is strictly below the squared distance to the
+// outer faces of the block (every cell outside lies beyond a face) and no
+// other entry ties it and no bucket holds more than 8 entries; else
+// sh.any_full is set.  `skip` = the killed slot; slot `moved` is taken at
+// (mx,my,mz) instead of its stored site.
+__device__ void grid_search(const DevChain &d, Shared &sh, int nq, int skip, int moved, double mx, double my,
+                            double mz) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const CellGrid &G = d.grid;
+    if (tid == 0) sh.any_full = 0;
+    if (wv < nq) {
+        const double x = sh.qx[wv], y = sh.qy[wv], z = sh.qz[wv];
+        const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
+                  bk = grid_axis(z, G.z0, G.iz, G.gz);
+        const int nb = lane % 27, grp = lane / 27;
+        const int ii = bi + nb % 3 - 1, jj = bj + (nb / 3) % 3 - 1, kk = bk + nb / 9 - 1;
+        const bool inb = lane < 54 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
+        const int b = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
+        const int cnt = d.bucket_count[b];
+        BucketEntry e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = d.buckets[b * kBucketCap + grp * 4 + u];
+        double bd = kSentinel;
+        int bs = -1;
+        bool tie = false, overfull = inb && cnt > 8;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool ok = inb && grp * 4 + u < cnt && e[u].slot != skip && e[u].slot != moved;
+            const double dd = dist2(e[u].x, e[u].y, e[u].z, x, y, z);
+            if (ok) {
+                if (dd < bd) {
+                    bd = dd;
+                    bs = e[u].slot;
+                    tie = false;
+                } else if (dd == bd && dd < kSentinel) {
+                    tie = true;
+                }
+            }
+        }
+        if (lane == 63 && moved >= 0) {  // the moved cell, at its proposed site
+            const double dd = dist2(mx, my, mz, x, y, z);
+            if (dd < bd) {
+                bd = dd;
+                bs = moved;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double od = __shfl_xor(bd, off, 64);
+            const int os = __shfl_xor(bs, off, 64);
+            const bool ot = __shfl_xor((int)tie, off, 64) != 0;
+            if (od < bd) {
+                bd = od;
+                bs = os;
+                tie = ot;
+            } else if (od == bd && od < kSentinel && os != bs) {
+                tie = true;
+            } else if (od == bd) {
+                tie = tie || ot;
+            }
+        }
+        const bool any_over = __ballot(overfull) != 0ull;
+        if (lane == 0) {
+            // squared distance to the nearest outer face of the searched block
+            double lb = __builtin_huge_val();
+            auto face = [&lb](double v, double v0, double inv, double h, int g) {
+                const int i = grid_axis(v, v0, inv, g);
+                if (i - 1 > 0) {
+                    const double gap = v - (v0 + (double)(i - 1) * h);
+                    lb = gap > 0.0 ? fmin(lb, gap * gap) : 0.0;
+                }
+                if (i + 1 < g - 1) {
+                    const double gap = (v0 + (double)(i + 2) * h) - v;
+                    lb = gap > 0.0 ? fmin(lb, gap * gap) : 0.0;
+                }
+            };
+            face(x, G.x0, G.ix, G.hx, G.gx);
+            face(y, G.y0, G.iy, G.hy, G.gy);
+            face(z, G.z0, G.iz, G.hz, G.gz);
+            // the relative margin covers the rounding of bucket indices vs faces
+            const bool proven = *d.grid_overflow == 0 && !tie && !any_over && bd < lb * (1.0 - 1e-9);
+            sh.res_d[wv] = bd;
+            sh.res_s[wv] = bd < kSentinel ? bs : -1;
+            sh.res_z[wv] = bd < kSentinel ? d.czeta[bs] : 0.0;
+            if (!proven) atomicOr(&sh.any_full, 1);
+        }
+    }
+    __syncthreads();
+}
+
+// Nearest live cell for nq query points: grid first, full scan if unproven.
+__device__ void nearest_queries(const DevChain &d, const Views &v, Shared &sh, int nq, int skip, int moved,
+                                double mx, double my, double mz) {
+    grid_search(d, sh, nq, skip, moved, mx, my, mz);
+    if (sh.any_full) {
+        if (threadIdx.x == 0) sh.grid_fallbacks += 1;
+        block_search(d, v, sh, nq, skip, moved, mx, my, mz);
+    }
+}
+
+// Apply the pending bucket-grid update (one wave).
+__device__ void grid_apply(const DevChain &d, Shared &sh, int lane) {
+    const int op = sh.g_op;
+    if (op & 1) {  // remove g_slot from the bucket of its old site
+        const int b = grid_bucket(d.grid, sh.g_ox, sh.g_oy, sh.g_oz);
+        const int cnt = d.bucket_count[b];
+        const int s = lane < kBucketCap ? d.buckets[b * kBucketCap + lane].slot : -1;
+        const unsigned long long m = __ballot(lane < cnt && s == sh.g_slot);
+        if (lane == 0) {
+            if (m == 0ull) {
+                *d.grid_overflow = 1;  // bookkeeping lost track: stop trusting the grid
+            } else {
+                d.buckets[b * kBucketCap + __builtin_ctzll(m)] = d.buckets[b * kBucketCap + cnt - 1];
+                d.bucket_count[b] = cnt - 1;
+            }
+        }
+    }
+    if ((op & 2) && lane == 0) {  // insert at the new site
+        const int b = grid_bucket(d.grid, sh.g_nx, sh.g_ny, sh.g_nz);
+        const int cnt = d.bucket_count[b];
+        if (cnt < kBucketCap) {
+            d.buckets[b * kBucketCap + cnt] = BucketEntry{sh.g_nx, sh.g_ny, sh.g_nz, sh.g_slot, 0};
+            d.bucket_count[b] = cnt + 1;
+        } else {
+            *d.grid_overflow = 1;
         }
     }
 }
 
-struct Shared {
-    Proposal p;
-    double czeta, zeta_killed, zetanew_death, kx, ky, kz, phi_n;
-    int slot_k, new_slot, ncells, accept;
-    int n_tiles, n_changed, n_orphans, n_rays, k0;
-    int pts_seen, ray_pts;  // roofline accounting
-    double red_d[kChainThreads / 64];
-    int red_j[kChainThreads / 64];
-};
-
-__device__ __forceinline__ void mark(const DevChain &d, Shared &sh, int p, int s, double dd, double z) {
+__device__ __forceinline__ void mark(const DevChain &d, const Views &v, Shared &sh, int p, int s, double dd,
+                                     double z) {
     d.cand_s[p] = s;
     d.cand_d[p] = dd;
     d.cand_z[p] = z;
     d.cand_flag[p] = 1;
     d.changed[atomicAdd(&sh.n_changed, 1)] = p;
+    const int r = d.pt_ray[p];
+    if (atomicExch(&v.rflag[r], 1) == 0) {
+        v.rhit[atomicAdd(&sh.n_rays, 1)] = r;
+        atomicMin(&sh.k0, r);
+    }
 }
 
-// Interpolation (MCsub.jl:306-327) of ONE point over the current cells by the
-// whole workgroup; cell at position `skip` is left out (the model after a
-// death).  Returns on all threads after a barrier: sh.red_j[0] = position.
-__device__ void block_nearest(const DevChain &d, Shared &sh, int ncells, int skip, double qx, double qy,
-                              double qz) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    double bd = kSentinel;
-    int bj = INT_MAX;
-    for (int j = tid; j < ncells; j += kChainThreads) {
-        if (j == skip) continue;
-        const int s = d.order[j];
-        const double dd = dist2(d.cx[s], d.cy[s], d.cz[s], qx, qy, qz);
-        if (dd < bd) {  // per thread j increases: first minimum kept
-            bd = dd;
-            bj = j;
-        }
-    }
-    wave_min_dj(bd, bj);
-    if (lane == 0) {
-        sh.red_d[wv] = bd;
-        sh.red_j[wv] = bj;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        for (int w = 1; w < kChainThreads / 64; ++w)
-            if (sh.red_d[w] < bd || (sh.red_d[w] == bd && sh.red_j[w] < bj)) {
-                bd = sh.red_d[w];
-                bj = sh.red_j[w];
-            }
-        sh.red_d[0] = bd;
-        sh.red_j[0] = bj;
-    }
-    __syncthreads();
+// Lower bound of dist2(q, p) over every point p of a tile.  The box is rounded
+// outward to FP32 and the gaps are computed in FP64 with the same rounded
+// operations as the distance, so lb2 <= dist2 holds bit-wise.
+__device__ __forceinline__ double tile_lb2(const float *lo, const float *hi, int nt, int t, double qx, double qy,
+                                           double qz) {
+    auto gap = [](double q, double l, double h) { return q < l ? l - q : (q > h ? q - h : 0.0); };
+    const double gx = gap(qx, (double)lo[t], (double)hi[t]);
+    const double gy = gap(qy, (double)lo[nt + t], (double)hi[nt + t]);
+    const double gz = gap(qz, (double)lo[2 * nt + t], (double)hi[2 * nt + t]);
+    double s = gx * gx;
+    s = s + gy * gy;
+    s = s + gz * gz;
+    return s;
 }
 
-__global__ __launch_bounds__(kChainThreads) void k_chain_run(DevChain d, long long iters) {
-    __shared__ Shared sh;
-    __shared__ double ray_scratch[kChainThreads / 64][96];
-    __shared__ double chi_t[2048];
+template <bool SMALL>
+__global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters) {
+    const DevChain &d = *dptr;  // fields read from memory as needed, not pinned in registers
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    Shared &sh = *reinterpret_cast<Shared *>(lds);
+    const LdsPlan L = lds_plan(d.ntiles, d.n, d.cap, SMALL);
+    double(*ray_scratch)[96] = reinterpret_cast<double(*)[96]>(lds + L.scratch);
+    tdchain::Draws *draws = reinterpret_cast<tdchain::Draws *>(lds + L.draws);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    constexpr int kWaves = kChainThreads / 64;
     const tdchain::Params &P = d.params;
-    ChainScalars *st = d.st;
+    const int n = d.n, NT = d.ntiles;
+    const bool prof_on = d.profile != 0;
+    const int chi_chunk = SMALL ? n : 2048;
+
+    // ---- views: LDS copies of the tile / ray / order arrays when they fit ----
+    Views v;
+    v.tlo = d.tile_lo; v.thi = d.tile_hi; v.tmaxd = d.tile_maxd; v.tstart = d.tile_start; v.thit = d.tiles_hit;
+    v.ray_off = d.ray_off; v.ptS = d.ptS; v.prefix = d.prefix; v.cptS = d.cand_ptS; v.cprefix = d.cand_prefix;
+    v.tS = d.tS; v.sig = d.sig; v.rflag = d.ray_flag; v.rhit = d.rays_hit; v.ord = d.order;
+    v.chi = reinterpret_cast<double *>(lds + L.chi);
+    if constexpr (SMALL) {
+        float *a = reinterpret_cast<float *>(lds + L.tlo), *b = reinterpret_cast<float *>(lds + L.thi);
+        double *m = reinterpret_cast<double *>(lds + L.tmaxd);
+        int *ts = reinterpret_cast<int *>(lds + L.tstart), *ro = reinterpret_cast<int *>(lds + L.rayoff);
+        double *p = reinterpret_cast<double *>(lds + L.ptS), *pf = reinterpret_cast<double *>(lds + L.prefix);
+        double *t = reinterpret_cast<double *>(lds + L.tS), *sg = reinterpret_cast<double *>(lds + L.sig);
+        int *rf = reinterpret_cast<int *>(lds + L.rflag), *od = reinterpret_cast<int *>(lds + L.ord);
+        for (int i = tid; i < 3 * NT; i += kChainThreads) {
+            a[i] = d.tile_lo[i];
+            b[i] = d.tile_hi[i];
+        }
+        for (int i = tid; i < NT; i += kChainThreads) m[i] = d.tile_maxd[i];
+        for (int i = tid; i <= NT; i += kChainThreads) ts[i] = d.tile_start[i];
+        for (int i = tid; i <= n; i += kChainThreads) ro[i] = d.ray_off[i];
+        for (int i = tid; i < n; i += kChainThreads) {
+            p[i] = d.ptS[i];
+            pf[i] = d.prefix[i];
+            t[i] = d.tS[i];
+            sg[i] = d.sig[i];
+            rf[i] = 0;
+        }
+        for (int i = tid; i < d.cap; i += kChainThreads) od[i] = d.order[i];
+        v.tlo = a; v.thi = b; v.tmaxd = m; v.tstart = ts; v.ray_off = ro; v.ptS = p; v.prefix = pf; v.tS = t;
+        v.sig = sg; v.rflag = rf; v.ord = od;
+        v.cptS = reinterpret_cast<double *>(lds + L.cptS);
+        v.cprefix = reinterpret_cast<double *>(lds + L.cprefix);
+        v.thit = reinterpret_cast<int *>(lds + L.thit);
+        v.rhit = reinterpret_cast<int *>(lds + L.rhit);
+    }
+    if (tid == 0) {
+        const ChainScalars &s0 = *d.st;
+        sh.iter = s0.iter;
+        sh.evaluations = 0;
+        sh.bytes = 0;
+        sh.grid_fallbacks = 0;
+        for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
+        sh.phi = s0.phi;
+        sh.ncells = s0.ncells;
+        sh.nslots = s0.nslots;
+        sh.nfree = s0.nfree;
+        sh.clr_changed = sh.clr_rays = 0;
+        sh.g_op = 0;
+        for (int k = 0; k < 16; ++k) sh.prof[k] = 0;
+        sh.t_last = clock64();
+    }
+    __syncthreads();
 
     for (long long it = 0; it < iters; ++it) {
-        // ---------------- draw the proposal (one lane) ----------------
+        // ---- the RNG draws (and their normal quantiles) of the next 64
+        //      iterations, one lane each: a function of (seed, chain, iteration) ----
+        if ((it & 63) == 0) {
+            if (wv == 0) draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
+            __syncthreads();
+        }
+        // ================= phase A: housekeeping + draw =================
+        for (int c = tid; c < sh.clr_changed; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
+        for (int c = tid; c < sh.clr_rays; c += kChainThreads) v.rflag[v.rhit[c]] = 0;
+        if (wv == kWaves - 1 && sh.g_op) {
+            grid_apply(d, sh, lane);
+            if (lane == 0) sh.g_op = 0;
+        }
         if (tid == 0) {
-            const int ncells = st->ncells;
-            const tdchain::Draws dr = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)st->iter);
+            const int ncells = sh.ncells;
+            const tdchain::Draws dr = draws[it & 63];
             Proposal p = tdchain::propose(P, dr, ncells);
             sh.slot_k = -1;
             sh.new_slot = -1;
             if (p.active && p.action != tdchain::kBirth) {
-                const int s = d.order[p.index];
+                const int s = v.ord[p.index];
+                const double x = d.cx[s], y = d.cy[s], z = d.cz[s], ze = d.czeta[s];
                 sh.slot_k = s;
-                sh.kx = d.cx[s];
-                sh.ky = d.cy[s];
-                sh.kz = d.cz[s];
-                sh.zeta_killed = d.czeta[s];
-                tdchain::complete_proposal(P, dr, p, d.cx[s], d.cy[s], d.cz[s], d.czeta[s]);
+                sh.kx = x;
+                sh.ky = y;
+                sh.kz = z;
+                sh.zeta_killed = ze;
+                tdchain::complete_proposal(P, dr, p, x, y, z, ze);
             }
             if (p.active && p.action == tdchain::kBirth)
-                sh.new_slot = st->nfree > 0 ? d.free_slots[st->nfree - 1] : st->nslots;
-            if (p.active) st->proposed[p.action] += 1;
+                sh.new_slot = sh.nfree > 0 ? d.free_slots[sh.nfree - 1] : sh.nslots;
+            if (p.active) sh.proposed[p.action] += 1;
+            if (p.active && (p.action == tdchain::kBirth || p.action == tdchain::kDeath)) {
+                sh.qx[0] = p.action == tdchain::kBirth ? p.x : sh.kx;
+                sh.qy[0] = p.action == tdchain::kBirth ? p.y : sh.ky;
+                sh.qz[0] = p.action == tdchain::kBirth ? p.z : sh.kz;
+            }
             sh.p = p;
-            sh.ncells = ncells;
+            // forward evaluation needed (birth validity is only known after its query)
+            sh.eval = p.active && (p.valid || p.action == tdchain::kBirth) && P.debug_prior != 1;
             sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
             sh.pts_seen = sh.ray_pts = 0;
-            sh.k0 = d.n;
+            sh.k0 = n;
             sh.accept = 0;
         }
         __syncthreads();
+        STAMP(0);
         const int action = sh.p.action;
         const int ncells = sh.ncells;
         if (sh.p.active) {
-            // -------- 1-point Interpolations of the birth/death branches --------
-            if (action == tdchain::kBirth || action == tdchain::kDeath) {
-                const bool birth = action == tdchain::kBirth;
-                block_nearest(d, sh, ncells, birth ? -1 : (int)sh.p.index, birth ? sh.p.x : sh.kx,
-                              birth ? sh.p.y : sh.ky, birth ? sh.p.z : sh.kz);
-                if (tid == 0) {
-                    st->bytes += (int64_t)ncells * 28;  // order + coordinates of every cell
-                    const int j = sh.red_j[0];
-                    const double v = (j != INT_MAX) ? d.czeta[d.order[j]] : 0.0;
-                    if (birth) {
-                        sh.czeta = v;  // TD_inversion_function.jl:81
-                        tdchain::birth_zeta(P, sh.p, v);
-                    } else {
-                        sh.zetanew_death = v;  // :146
-                    }
+            Proposal p = sh.p;
+            const int slot_k = sh.slot_k;
+            const bool eval = sh.eval;
+            const double kx = sh.kx, ky = sh.ky, kz = sh.kz;
+            // ============ phase B: tile pass || birth/death Interpolation ============
+            if (eval) {
+                const bool q0 = action != tdchain::kBirth;  // old site of the selected cell
+                const bool q1 = action == tdchain::kBirth || action == tdchain::kMove;  // new site
+                for (int t = tid; t < NT; t += kChainThreads) {
+                    const double mx = v.tmaxd[t];
+                    bool hit = false;
+                    if (q0) hit = tile_lb2(v.tlo, v.thi, NT, t, kx, ky, kz) <= mx;
+                    if (q1 && !hit) hit = tile_lb2(v.tlo, v.thi, NT, t, p.x, p.y, p.z) <= mx;
+                    if (hit) v.thit[atomicAdd(&sh.n_tiles, 1)] = t;
                 }
-                __syncthreads();
             }
-            if (sh.p.valid) {
-                if (P.debug_prior == 1) {
-                    if (tid == 0) sh.phi_n = 1.0;  // MCsub.jl:134-136
+            if (action == tdchain::kDeath)  // deleteat! shift, staged before we know if it is accepted
+                for (int j = (int)p.index + 1 + tid; j < ncells; j += kChainThreads) d.order_tmp[j] = v.ord[j];
+            double czeta = 0.0, zetanew_death = 0.0;
+            if (action == tdchain::kBirth || action == tdchain::kDeath) {
+                nearest_queries(d, v, sh, 1, action == tdchain::kDeath ? slot_k : -1, -1, 0.0, 0.0, 0.0);
+                if (action == tdchain::kBirth) {
+                    czeta = sh.res_z[0];                // TD_inversion_function.jl:81
+                    tdchain::birth_zeta(P, p, czeta);  // every lane, same value: no extra barrier
                 } else {
-                    const Proposal p = sh.p;
-                    const int slot_k = sh.slot_k;
-                    const bool q0 = action != tdchain::kBirth;  // old site of the selected cell
-                    const bool q1 = action == tdchain::kBirth || action == tdchain::kMove;  // new site
-                    // ---------------- tiles that may hold affected points ----------------
-                    for (int t = tid; t < d.ntiles; t += kChainThreads) {
-                        const double mx = d.tile_maxd[t];
-                        bool hit = false;
-                        if (q0) hit = tile_lb2(d, t, sh.kx, sh.ky, sh.kz) <= mx;
-                        if (q1 && !hit) hit = tile_lb2(d, t, p.x, p.y, p.z) <= mx;
-                        if (hit) d.tiles_hit[atomicAdd(&sh.n_tiles, 1)] = t;
-                    }
-                    __syncthreads();
-                    // ---------------- affected points ----------------
+                    zetanew_death = sh.res_z[0];  // :146
+                }
+            } else {
+                __syncthreads();  // tile list complete
+            }
+            STAMP(1);
+            if (p.valid) {
+                double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
+                if (P.debug_prior != 1) {
+                    // ================= phase C: affected points =================
                     const int nt = sh.n_tiles;
                     const int rank_k = slot_k >= 0 ? d.rank[slot_k] : 0;
+                    const double zeta_k = slot_k >= 0 ? d.czeta[slot_k] : 0.0;
                     int seen = 0;
                     for (int item = tid; item < nt * kTilePts; item += kChainThreads) {
-                        const int t = d.tiles_hit[item / kTilePts];
-                        const int q = d.tile_start[t] + item % kTilePts;
-                        if (q >= d.tile_start[t + 1]) continue;
+                        const int t = v.thit[item / kTilePts];
+                        const int q = v.tstart[t] + item % kTilePts;
+                        if (q >= v.tstart[t + 1]) continue;
                         ++seen;
                         const int s = d.best_s[q];
                         const double bd = d.best_d[q];
                         if (action == tdchain::kBirth) {  // appended cell: strict capture
                             const double dd = dist2(p.x, p.y, p.z, d.px[q], d.py[q], d.pz[q]);
-                            if (dd < bd) mark(d, sh, q, sh.new_slot, dd, p.zeta);
+                            if (dd < bd) mark(d, v, sh, q, sh.new_slot, dd, p.zeta);
                         } else if (action == tdchain::kChange) {
-                            if (s == slot_k) mark(d, sh, q, s, bd, p.zeta);
+                            if (s == slot_k) mark(d, v, sh, q, s, bd, p.zeta);
                         } else if (s == slot_k) {  // death / move: its points are re-searched
                             d.orphans[atomicAdd(&sh.n_orphans, 1)] = q;
                         } else if (action == tdchain::kMove) {
                             const double dd = dist2(p.x, p.y, p.z, d.px[q], d.py[q], d.pz[q]);
                             if (dd < bd || (dd == bd && s >= 0 && rank_k < d.rank[s]))
-                                mark(d, sh, q, slot_k, dd, d.czeta[slot_k]);
+                                mark(d, v, sh, q, slot_k, dd, zeta_k);
                         }
                     }
                     if (seen) atomicAdd(&sh.pts_seen, seen);
                     __syncthreads();
-                    // ---------------- re-search orphaned points, one wave each ----------------
+                    STAMP(2);
+                    // ========= phase D: re-search orphaned points, one wave each =========
                     const int no = sh.n_orphans;
                     const bool death = action == tdchain::kDeath;
-                    for (int o = wv; o < no; o += kWaves) {
-                        const int q = d.orphans[o];
-                        const double x = d.px[q], y = d.py[q], z = d.pz[q];
-                        double bd = kSentinel;
-                        int bj = INT_MAX;
-                        for (int j = lane; j < ncells; j += 64) {
-                            if (death && j == (int)p.index) continue;
-                            const int s = d.order[j];
-                            double dd;
-                            if (s == slot_k)  // the moved cell at its proposed site
-                                dd = dist2(p.x, p.y, p.z, x, y, z);
-                            else
-                                dd = dist2(d.cx[s], d.cy[s], d.cz[s], x, y, z);
-                            if (dd < bd) {
-                                bd = dd;
-                                bj = j;
-                            }
+                    for (int o0 = 0; o0 < no; o0 += kBatch) {
+                        const int nq = min(kBatch, no - o0);
+                        if (tid < nq) {
+                            const int q = d.orphans[o0 + tid];
+                            sh.qx[tid] = d.px[q];
+                            sh.qy[tid] = d.py[q];
+                            sh.qz[tid] = d.pz[q];
                         }
-                        wave_min_dj(bd, bj);
-                        if (lane == 0) {
-                            if (bj != INT_MAX) {
-                                const int s = d.order[bj];
-                                mark(d, sh, q, s, bd, d.czeta[s]);
-                            } else {
-                                mark(d, sh, q, -1, kSentinel, 0.0);
-                            }
-                        }
+                        __syncthreads();
+                        nearest_queries(d, v, sh, nq, death ? slot_k : -1, death ? -1 : slot_k, p.x, p.y, p.z);
+                        if (tid < nq)
+                            mark(d, v, sh, d.orphans[o0 + tid], sh.res_s[tid], sh.res_d[tid], sh.res_z[tid]);
+                        __syncthreads();
                     }
-                    __syncthreads();
-                    // ---------------- rays holding changed points ----------------
-                    const int nc = sh.n_changed;
-                    for (int c = tid; c < nc; c += kChainThreads) {
-                        const int r = d.pt_ray[d.changed[c]];
-                        if (atomicExch(&d.ray_flag[r], 1) == 0) {
-                            d.rays_hit[atomicAdd(&sh.n_rays, 1)] = r;
-                            atomicMin(&sh.k0, r);
-                        }
-                    }
-                    __syncthreads();
+                    STAMP(3);
+                    // ================= phase E: t* of the rays that changed =================
                     const int nr = sh.n_rays;
                     const OverlayZeta oz{d.cand_flag, d.cand_z, d.zeta0};
                     for (int rr = wv; rr < nr; rr += kWaves) {
-                        const int r = d.rays_hit[rr];
-                        const int s0 = d.ray_off[r];
-                        const double v = wave_ray_sum(lane, d.w, oz, s0, d.ray_off[r + 1] - s0, ray_scratch[wv]);
+                        const int r = v.rhit[rr];
+                        const int s0 = v.ray_off[r];
+                        const int npr = v.ray_off[r + 1] - s0;
+                        const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
                         if (lane == 0) {
-                            d.cand_ptS[r] = v;
-                            atomicAdd(&sh.ray_pts, d.ray_off[r + 1] - s0);
+                            v.cptS[r] = val;
+                            atomicAdd(&sh.ray_pts, npr);
                         }
                     }
                     __syncthreads();
-                    // ---------------- chi^2 from the first changed ray on ----------------
+                    STAMP(4);
+                    // ========== phase F: chi^2 from the first changed ray on ==========
+                    // terms in parallel into LDS, then ONE lane adds them in k order
+                    // (MCsub.jl:170-172), 8 terms per LDS round trip
                     const int k0 = sh.k0;
-                    double C = k0 > 0 ? d.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
-                    for (int base = k0; base < d.n; base += 2048) {
-                        const int cnt = min(2048, d.n - base);
+                    double C = (tid == 0 && k0 > 0) ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
+                    for (int base = k0; base < n; base += chi_chunk) {
+                        const int cnt = min(chi_chunk, n - base);
                         for (int k = tid; k < cnt; k += kChainThreads) {
                             const int r = base + k;
-                            const double pt = d.ray_flag[r] ? d.cand_ptS[r] : d.ptS[r];
-                            const double df = pt - d.tS[r];
-                            const double sg = d.sig[r];
-                            chi_t[k] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
+                            const double pt = v.rflag[r] ? v.cptS[r] : v.ptS[r];
+                            const double df = pt - v.tS[r];
+                            const double sg = v.sig[r];
+                            v.chi[k] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                         }
                         __syncthreads();
-                        if (tid == 0)
-                            for (int k = 0; k < cnt; ++k) {
-                                C = C + chi_t[k];
-                                d.cand_prefix[base + k] = C;
+                        if (tid == 0) {
+                            int k = 0;
+                            for (; k + 8 <= cnt; k += 8) {
+                                double t[8], c[8];
+#pragma unroll
+                                for (int u = 0; u < 8; ++u) t[u] = v.chi[k + u];
+#pragma unroll
+                                for (int u = 0; u < 8; ++u) {
+                                    C = C + t[u];
+                                    c[u] = C;
+                                }
+#pragma unroll
+                                for (int u = 0; u < 8; ++u) v.cprefix[base + k + u] = c[u];
                             }
-                        __syncthreads();
+                            for (; k < cnt; ++k) {
+                                C = C + v.chi[k];
+                                v.cprefix[base + k] = C;
+                            }
+                        }
+                        if (base + chi_chunk < n) __syncthreads();  // the LDS terms are reused
                     }
+                    phi_n = k0 < n ? C : sh.phi;
                     if (tid == 0) {
-                        sh.phi_n = k0 < d.n ? C : st->phi;
-                        st->evaluations += 1;
-                        // bytes this proposal's algorithm must read: tile boxes + maxima (56 B),
-                        // candidate points (coords + cached slot/distance, 36 B), orphan scans
-                        // (order + coords per cell, 28 B), rays (w, zeta, flag: 17 B per point),
+                        sh.evaluations += 1;
+                        // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
+                        // candidate points (coords + cached slot/distance, 36 B), grid queries
+                        // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
                         // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
-                        st->bytes += (int64_t)d.ntiles * 56 + (int64_t)sh.pts_seen * 36 +
-                                     (int64_t)sh.n_orphans * ncells * 28 + (int64_t)sh.ray_pts * 17 +
-                                     (int64_t)(d.n - k0) * 28;
+                        sh.bytes += (long long)NT * 32 + (long long)sh.pts_seen * 36 +
+                                    (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
+                                    (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28;
                     }
                 }
-                __syncthreads();
-                // ---------------- Metropolis-Hastings decision ----------------
+                // ================= Metropolis-Hastings decision =================
                 if (tid == 0) {
-                    const bool acc = tdchain::accept(P, sh.p, ncells, st->phi, sh.phi_n, sh.czeta, sh.zeta_killed,
-                                                     sh.zetanew_death);
+                    const bool acc = tdchain::accept(P, p, ncells, sh.phi, phi_n, czeta, sh.zeta_killed,
+                                                     zetanew_death);
                     sh.accept = acc ? 1 : 0;
-                    if (acc) st->accepted[action] += 1;
+                    sh.phi_n = phi_n;
+                    if (acc) sh.accepted[action] += 1;
                 }
                 __syncthreads();
-                const int nc = sh.n_changed, nr = sh.n_rays, nt = sh.n_tiles;
+                STAMP(5);
+                // ================= phase G: commit =================
                 if (sh.accept) {
-                    // -------- commit: points, rays, chi^2 prefix, cells --------
+                    const int nc = sh.n_changed, nr = sh.n_rays, nt = sh.n_tiles, k0 = sh.k0;
                     for (int c = tid; c < nc; c += kChainThreads) {
                         const int q = d.changed[c];
                         d.best_s[q] = d.cand_s[q];
                         d.best_d[q] = d.cand_d[q];
                         d.zeta0[q] = d.cand_z[q];
-                        d.cand_flag[q] = 0;
                     }
+                    // tile maxima of the new distances (changed points lie in hit tiles;
+                    // the overlay reads the new value whether or not it is committed yet)
+                    if (P.debug_prior != 1 && action != tdchain::kChange)
+                        for (int i = tid; i < nt * kTilePts; i += kChainThreads) {  // 16 lanes per tile
+                            const int t = v.thit[i / kTilePts];
+                            const int q = v.tstart[t] + (i % kTilePts);
+                            double mx = -1.0;
+                            if (q < v.tstart[t + 1]) mx = d.cand_flag[q] ? d.cand_d[q] : d.best_d[q];
+#pragma unroll
+                            for (int off = kTilePts / 2; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
+                            if ((i % kTilePts) == 0) v.tmaxd[t] = mx;
+                        }
                     for (int rr = tid; rr < nr; rr += kChainThreads) {
-                        const int r = d.rays_hit[rr];
-                        d.ptS[r] = d.cand_ptS[r];
-                        d.ray_flag[r] = 0;
+                        const int r = v.rhit[rr];
+                        v.ptS[r] = v.cptS[r];
                     }
-                    for (int r = sh.k0 + tid; r < d.n; r += kChainThreads) d.prefix[r] = d.cand_prefix[r];
-                    const Proposal p = sh.p;
-                    if (action == tdchain::kDeath) {  // deleteat!: positions after the killed one shift down
-                        for (int j = (int)p.index + 1 + tid; j < ncells; j += kChainThreads) d.order_tmp[j] = d.order[j];
-                        __syncthreads();
+                    for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
+                    if (action == tdchain::kDeath)  // deleteat!: positions after the killed one shift down
                         for (int j = (int)p.index + 1 + tid; j < ncells; j += kChainThreads) {
                             const int s = d.order_tmp[j];
-                            d.order[j - 1] = s;
+                            v.ord[j - 1] = s;
                             d.rank[s] = j - 1;
                         }
-                    }
                     if (tid == 0) {
                         const int sk = sh.slot_k;
                         if (action == tdchain::kBirth) {  // append!
@@ -355,45 +705,78 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(DevChain d, long lo
                             d.cy[s] = p.y;
                             d.cz[s] = p.z;
                             d.czeta[s] = p.zeta;
-                            d.order[ncells] = s;
+                            v.ord[ncells] = s;
                             d.rank[s] = ncells;
-                            if (st->nfree > 0)
-                                st->nfree -= 1;
+                            if (sh.nfree > 0)
+                                sh.nfree -= 1;
                             else
-                                st->nslots += 1;
-                            st->ncells = ncells + 1;
+                                sh.nslots += 1;
+                            sh.ncells = ncells + 1;
+                            sh.g_op = 2;
+                            sh.g_slot = s;
                         } else if (action == tdchain::kDeath) {
-                            d.free_slots[st->nfree] = sk;
-                            st->nfree += 1;
+                            d.free_slots[sh.nfree] = sk;
+                            sh.nfree += 1;
                             d.rank[sk] = -1;
-                            st->ncells = ncells - 1;
+                            sh.ncells = ncells - 1;
+                            sh.g_op = 1;
+                            sh.g_slot = sk;
                         } else if (action == tdchain::kChange) {
                             d.czeta[sk] = p.zeta;
                         } else {
                             d.cx[sk] = p.x;
                             d.cy[sk] = p.y;
                             d.cz[sk] = p.z;
+                            sh.g_op = 3;
+                            sh.g_slot = sk;
                         }
-                        st->phi = sh.phi_n;
+                        sh.g_ox = sh.kx;
+                        sh.g_oy = sh.ky;
+                        sh.g_oz = sh.kz;
+                        sh.g_nx = p.x;
+                        sh.g_ny = p.y;
+                        sh.g_nz = p.z;
+                        sh.phi = sh.phi_n;
                     }
-                    __syncthreads();
-                    // tile maxima of the committed distances (changed points lie in hit tiles)
-                    if (P.debug_prior != 1)
-                        for (int i = tid; i < nt; i += kChainThreads) {
-                            const int t = d.tiles_hit[i];
-                            double mx = -1.0;
-                            for (int q = d.tile_start[t]; q < d.tile_start[t + 1]; ++q) mx = fmax(mx, d.best_d[q]);
-                            d.tile_maxd[t] = mx;
-                        }
-                } else {
-                    for (int c = tid; c < nc; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
-                    for (int rr = tid; rr < nr; rr += kChainThreads) d.ray_flag[d.rays_hit[rr]] = 0;
                 }
             }
         }
+        if (tid == 0) {
+            sh.iter += 1;
+            sh.clr_changed = sh.n_changed;
+            sh.clr_rays = sh.n_rays;
+        }
         __syncthreads();
-        if (tid == 0) st->iter += 1;
-        __syncthreads();
+        STAMP(6);
+    }
+
+    // ---- leave a clean state behind: flags, pending grid update, LDS copies ----
+    for (int c = tid; c < sh.clr_changed; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
+    for (int c = tid; c < sh.clr_rays; c += kChainThreads) v.rflag[v.rhit[c]] = 0;
+    if (wv == kWaves - 1 && sh.g_op) grid_apply(d, sh, lane);
+    if constexpr (SMALL) {
+        for (int i = tid; i < NT; i += kChainThreads) d.tile_maxd[i] = v.tmaxd[i];
+        for (int i = tid; i < n; i += kChainThreads) {
+            d.ptS[i] = v.ptS[i];
+            d.prefix[i] = v.prefix[i];
+        }
+        for (int i = tid; i < sh.ncells; i += kChainThreads) d.order[i] = v.ord[i];
+    }
+    if (tid == 0) {
+        ChainScalars &s = *d.st;
+        s.iter = sh.iter;
+        s.evaluations += sh.evaluations;
+        s.bytes += sh.bytes;
+        for (int a = 0; a < 5; ++a) {
+            s.proposed[a] += sh.proposed[a];
+            s.accepted[a] += sh.accepted[a];
+        }
+        s.phi = sh.phi;
+        s.ncells = sh.ncells;
+        s.nslots = sh.nslots;
+        s.nfree = sh.nfree;
+        for (int k = 0; k < 15; ++k) s.prof[k] += sh.prof[k];
+        s.prof[15] += sh.grid_fallbacks;  // diagnostic: unproven grid searches
     }
 }
 
@@ -431,6 +814,8 @@ __global__ void k_tile_max(const int *__restrict__ tile_start, int ntiles, const
     tile_maxd[t] = mx;
 }
 
+constexpr size_t kLdsBudget = 160 * 1024;
+
 }  // namespace
 
 hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, hipStream_t s) {
@@ -462,8 +847,17 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
     return e;
 }
 
-hipError_t chain_run(const DevChain &d, int64_t iters, hipStream_t s) {
-    hipLaunchKernelGGL(k_chain_run, dim3(1), dim3(kChainThreads), 0, s, d, (long long)iters);
+hipError_t chain_run(const DevChain &d, const DevChain *dptr, int64_t iters, hipStream_t s) {
+    const LdsPlan small = lds_plan(d.ntiles, d.n, d.cap, true);
+    if (small.total <= kLdsBudget) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_chain_run<true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)small.total);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_chain_run<true>, dim3(1), dim3(kChainThreads), small.total, s, dptr, (long long)iters);
+    } else {
+        const size_t lds = lds_plan(d.ntiles, d.n, d.cap, false).total;
+        hipLaunchKernelGGL(k_chain_run<false>, dim3(1), dim3(kChainThreads), lds, s, dptr, (long long)iters);
+    }
     return hipGetLastError();
 }
 

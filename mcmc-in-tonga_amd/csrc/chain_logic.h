@@ -59,7 +59,10 @@ enum Slot : uint32_t { kSlotAction = 0, kSlotXY = 1, kSlotZZeta = 2, kSlotIndex 
 
 struct Draws {
     double u_action, u_accept, u_a, u_b, u_c, u_zeta, u_index;
+    double z_a, z_b, z_c, z_zeta;  // standard-normal quantiles of u_a, u_b, u_c, u_zeta
 };
+
+TD_HD double normal_quantile(double p);
 
 TD_HD Draws draw_iteration(uint64_t seed, uint32_t chain, uint64_t iter) {
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -76,6 +79,12 @@ TD_HD Draws draw_iteration(uint64_t seed, uint32_t chain, uint64_t iter) {
     r.u_c = u01(c.x, c.y);
     r.u_zeta = u01(c.z, c.w);
     r.u_index = u01(d.x, d.y);
+    // the normals every branch may need, drawn up front: a pure function of the
+    // uniforms, so the device can precompute them for many iterations at once
+    r.z_a = normal_quantile(r.u_a);
+    r.z_b = normal_quantile(r.u_b);
+    r.z_c = normal_quantile(r.u_c);
+    r.z_zeta = normal_quantile(r.u_zeta);
     return r;
 }
 
@@ -212,7 +221,7 @@ struct Proposal {
     int64_t index;    // kill / change / move cell (0-based)
     double x, y, z;   // birth location / move target
     double zeta;      // change: new value (birth: filled after czeta is known)
-    double u_zeta;    // birth: uniform for zetanew ~ Normal(czeta, sig_zeta)
+    double z_zeta;    // birth: standard normal for zetanew ~ Normal(czeta, sig_zeta)
     double u_accept;
 };
 
@@ -223,7 +232,7 @@ TD_HD Proposal propose(const Params &P, const Draws &d, int64_t ncells) {
     p.action = 1 + (int)(d.u_action * 4.0);
     if (p.action > 4) p.action = 4;
     p.u_accept = d.u_accept;
-    p.u_zeta = d.u_zeta;
+    p.z_zeta = d.z_zeta;
     p.valid = 1;
     p.active = 1;
     switch (p.action) {
@@ -254,12 +263,12 @@ TD_HD void complete_proposal(const Params &P, const Draws &d, Proposal &p, doubl
                              double czeta) {
     if (!p.active) return;
     if (p.action == kChange) {
-        p.zeta = czeta + P.sig_zeta * normal_quantile(d.u_zeta);
+        p.zeta = czeta + P.sig_zeta * d.z_zeta;
         p.valid = (p.zeta > 0.0 && p.zeta < P.zeta_scale) ? 1 : 0;
     } else if (p.action == kMove) {
-        p.x = cx + P.xr * normal_quantile(d.u_a);
-        p.y = cy + P.yr * normal_quantile(d.u_b);
-        p.z = cz + P.zr * normal_quantile(d.u_c);
+        p.x = cx + P.xr * d.z_a;
+        p.y = cy + P.yr * d.z_b;
+        p.z = cz + P.zr * d.z_c;
         p.zeta = czeta;
         p.valid = (p.x >= P.xmin && p.x <= P.xmax && p.y >= P.ymin && p.y <= P.ymax && p.z >= P.zmin &&
                    p.z <= P.zmax) ? 1 : 0;
@@ -268,7 +277,7 @@ TD_HD void complete_proposal(const Params &P, const Draws &d, Proposal &p, doubl
 
 // Birth, once czeta = Interpolation(model, xNew, yNew, zNew) is known (:81-82, :92).
 TD_HD void birth_zeta(const Params &P, Proposal &p, double czeta) {
-    p.zeta = czeta + P.sig_zeta * normal_quantile(p.u_zeta);
+    p.zeta = czeta + P.sig_zeta * p.z_zeta;
     p.valid = (p.zeta > 0.0 && p.zeta < P.zeta_scale) ? 1 : 0;
 }
 

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Diagnostic: where one DEVICE-engine chain iteration spends its cycles.
+
+Runs the config-3 chain (381 rays x 5000 cells) with the kernel's s_memtime
+phase stamps enabled (a diagnostic mode; never used for bench numbers) and
+prints the per-phase share of shader cycles and cycles per iteration."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import tonga  # noqa: E402
+
+# k_chain_run phases A..G (chain_kernels.hip, STAMP(0..6))
+PHASES = ["A draw", "B tiles + birth/death query", "C points", "D orphans", "E ray sums", "F chi2 + accept",
+          "G commit"]
+
+
+def main():
+    N = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
+    tt = tonga.load()
+    ds = tt.load_data_Tonga()
+    ctx = tt.TdContext.from_datastruct(ds)
+    prm = tt.define_TDstructrure().replace(max_cells=2 * N)
+    ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000, chain=1), tt.random_model(N, 3))
+    ch.run(2000)
+    L = tt.lib()
+    out0 = (ctypes.c_int64 * 16)()
+    L.tdt_chain_profile(ch.h, 1, out0)
+    t0 = time.perf_counter()
+    ch.run(iters)
+    el = time.perf_counter() - t0
+    out = (ctypes.c_int64 * 16)()
+    L.tdt_chain_profile(ch.h, 0, out)
+    cyc = np.array(out[:7], dtype=np.float64) - np.array(out0[:7], dtype=np.float64)
+    fallbacks = int(out[15] - out0[15])
+    tot = cyc.sum()
+    res = {"cells": N, "iters": iters, "us_per_iter_wall": el / iters * 1e6,
+           "cycles_per_iter": tot / iters, "grid_fallbacks": fallbacks,
+           "phases": {p: {"share": round(c / tot, 4), "cycles_per_iter": round(c / iters, 1)}
+                      for p, c in zip(PHASES, cyc)}}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

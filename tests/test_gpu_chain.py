@@ -97,3 +97,26 @@ def test_reference_driver_thinning(tt, ds):
         m2 = m.copy()
         tt.evaluate(m2, ds, prm)
         assert m2.phi == m.phi
+
+
+def test_clustered_and_boundary_cells(tt, ds, ctx):
+    """Cells packed into one spot (bucket overflow -> full scans) and cells on
+    the box faces (clamped buckets): the device engine must still follow the
+    host engine bit for bit."""
+    xmin, xmax, ymin, ymax, zmin, zmax = tt.box()
+    rng = np.random.default_rng(3)
+    k = 120
+    x = np.concatenate([rng.uniform(400, 401, k), rng.choice([xmin, xmax], 40)])
+    y = np.concatenate([rng.uniform(100, 101, k), rng.uniform(ymin, ymax, 40)])
+    z = np.concatenate([rng.uniform(300, 301, k), rng.choice([zmin, zmax], 40)])
+    zeta = rng.uniform(1, 49, len(x))
+    x[5], y[5], z[5] = x[4], y[4], z[4]  # an exact duplicate
+    model = tt.Model(float(len(x)), x, y, z, zeta)
+    prm = tt.define_TDstructrure().replace(max_cells=400)
+    dev = make(tt, ctx, prm, model, 17, tt.TD_ENGINE_DEVICE)
+    host = make(tt, ctx, prm, model, 17, tt.TD_ENGINE_HOST)
+    for _ in range(3):
+        dev.run(200)
+        host.run(200)
+        assert dev.stats()["phi"] == host.stats()["phi"]
+    assert same_models(dev.model(), host.model())

@@ -123,13 +123,14 @@ def test_interpolate_matches_oracle(tt, orc, ctx):
     z, near = ctx.interpolate(cells, X, Y, Z, want_nearest=True)
     zr, ir = orc.interpolation(cells, X, Y, Z)
     assert np.array_equal(z, zr) and np.array_equal(near, ir)
+    z_first = zr[0]
     # broadcast Y/Z of length 1 (the xzMap / xyMap cross sections, MCsub.jl:317-322)
     Xn = np.concatenate([X[:50], [np.nan], X[50:60]])
     z, near = ctx.interpolate(cells, Xn, [150.0], [300.0], want_nearest=True)
     zr, ir = orc.interpolation(cells, Xn, [150.0], [300.0])
     assert len(z) == 50 and np.array_equal(z, zr) and np.array_equal(near, ir)
     # single point (birth / death queries)
-    assert tt.Interpolation(tt.define_TDstructrure(), tt.Model(800.0, *cells), [X[0]], [Y[0]], [Z[0]])[0] == zr[0]
+    assert tt.Interpolation(tt.define_TDstructrure(), tt.Model(800.0, *cells), [X[0]], [Y[0]], [Z[0]])[0] == z_first
     with pytest.raises(tt.TdError) as e:
         ctx.interpolate(cells, X[:5], Y[:2], Z[:5])
     assert e.value.code == 5
