@@ -53,6 +53,15 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full-evaluate", action="store_true")
+    ap.add_argument("--chains-per-gpu", type=int, default=1,
+                    help="independent chains per rank, one workgroup each, one launch (td_chain_run_batch)")
+    ap.add_argument("--swap-every", type=int, default=0,
+                    help="parallel tempering: exchange temperatures every K proposals (RCCL allgather); 0 = "
+                         "independent chains as the reference's pmap")
+    ap.add_argument("--tmax", type=float, default=8.0)
+    ap.add_argument("--batch-chains", type=int, default=256,
+                    help="size of the extra many-chains-per-GPU measurement on rank 0 (0 = skip)")
+    ap.add_argument("--batch-iters", type=int, default=1000)
     return ap.parse_args()
 
 
@@ -77,7 +86,31 @@ def main():
     model = tt.random_model(N, 3)  # config 3: seed 3
     ctx = tt.TdContext.from_datastruct(ds, device=local)
     prm = tt.define_TDstructrure().replace(max_cells=2 * N)
-    chain = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000 + rank, chain=1 + rank), model)
+    C = max(1, a.chains_per_gpu)
+    chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000 + rank * C + j, chain=1 + rank * C + j), model)
+              for j in range(C)]
+    ladder = None
+    if a.swap_every > 0:
+        ex = tt.Exchange(dist, "cuda") if dist is not None else tt.Exchange()
+        ladder = tt.TemperingLadder(chains, ex, tmax=a.tmax, seed=4242)
+
+    def run_step(k):
+        if ladder is not None:
+            done = 0
+            while done < k:
+                kk = min(a.swap_every, k - done)
+                ladder.step(kk)
+                done += kk
+        elif C > 1:
+            tt.run_batch(chains, k)
+        else:
+            chains[0].run(k)  # synchronous: returns after the kernel finished
+
+    def agg(key):
+        st = [c.stats() for c in chains]
+        if key in ("accepted", "proposed"):
+            return [sum(x[key][i] for x in st) for i in range(4)]
+        return sum(x[key] for x in st)
 
     def barrier_sync():
         if dist is not None:
@@ -87,16 +120,17 @@ def main():
             dist.barrier()
 
     for _ in range(a.warmup):
-        chain.run(a.iters_per_step)
-    s0 = chain.stats()
+        run_step(a.iters_per_step)
+    s0 = {k: agg(k) for k in ("accepted", "proposed", "bytes")}
     ctx.timing(enable=True, reset=True)
     barrier_sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        chain.run(a.iters_per_step)  # synchronous: returns after the kernel finished
+        run_step(a.iters_per_step)
     barrier_sync()
     el = time.perf_counter() - t0
-    s1 = chain.stats()
+    s1 = {k: agg(k) for k in ("accepted", "proposed", "bytes")}
+    s1["ncells"] = chains[0].stats()["ncells"]
     launches, kms = ctx.timing(kernel="chain_run")
     ctx.timing(enable=False)
     if dist is not None:
@@ -106,12 +140,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     iters = a.steps * a.iters_per_step
-    total = iters * world
+    total = iters * world * C
     value = total / el
     P = ctx.P
     acc = [x - y for x, y in zip(s1["accepted"], s0["accepted"])]
     prop = [x - y for x, y in zip(s1["proposed"], s0["proposed"])]
     nbytes = s1["bytes"] - s0["bytes"]
+    if ladder is not None:
+        launches = max(launches, 1)
     bytes_per_launch = nbytes / max(launches, 1)
     avg_s = kms / 1e3 / max(launches, 1)
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
@@ -128,9 +164,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "381 shipped rays (Data/381raypaths.jld), ak135 slowness substitute, synthetic seeded cells",
-        "config": {"workload": "config3: 381 rays x %d cells, 1 chain/GPU, birth/death/change/move" % N,
+        "config": {"workload": "config3: 381 rays x %d cells, %d chain/GPU, birth/death/change/move%s"
+                               % (N, C, ", tempering swap every %d (RCCL allgather)" % a.swap_every
+                                  if ladder is not None else ""),
                    "rays": int(ctx.n), "points": P, "cells_start": N, "cells_end": int(s1["ncells"]),
-                   "iters_per_step": a.iters_per_step, "engine": "device", "parallelism": "chains%d" % world},
+                   "iters_per_step": a.iters_per_step, "engine": "device",
+                   "parallelism": "chains%d" % (world * C)},
         # point x cell distance pairs a brute-force evaluate per proposal would need
         "nn_pair_evals_per_s_equiv": round(value * P * N, 1),
         "acceptance": {"birth/death/change/move accepted": acc, "proposed": prop,
@@ -141,17 +180,50 @@ def main():
                      "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
                      "note": "one persistent workgroup per chain: latency-bound by design (see DESIGN.md)"},
     }
+    if ladder is not None:
+        out["tempering"] = {"replicas": ladder.R, "temps": [round(t, 4) for t in ladder.temps],
+                            "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
     if rank == 0 and not a.no_full_evaluate:
         out["full_evaluate"] = full_evaluate(tt, ctx, model, N)
+    if rank == 0 and a.batch_chains > 0:
+        out["many_chains"] = many_chains(tt, ctx, ds, prm, model, a.batch_chains, a.batch_iters)
     if rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ds, model, a.cpu_seconds)
         if out["cpu_baseline"]["value"] > 0:
             out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
-    chain.close()
+    for c in chains:
+        c.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3):
+    """Occupancy mode (SURVEY 7 / 8d "batched multi-chain streams"): C
+    independent config-3 chains on this GPU, one workgroup each, one launch
+    per step.  Reported beside the headline, never as `value`."""
+    chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=50000 + j, chain=10000 + j), model) for j in range(C)]
+    tt.run_batch(chains, iters)  # warmup
+    b0 = sum(c.stats()["bytes"] for c in chains)
+    ctx.timing(enable=True, reset=True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tt.run_batch(chains, iters)
+    el = time.perf_counter() - t0
+    launches, kms = ctx.timing(kernel="chain_run")
+    ctx.timing(enable=False)
+    nbytes = sum(c.stats()["bytes"] for c in chains) - b0
+    for c in chains:
+        c.close()
+    value = C * iters * steps / el
+    achieved = nbytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+    return {"chains": C, "proposals_per_s": round(value, 1), "per_chain_proposals_per_s": round(value / C, 1),
+            "ms_per_launch": round(kms / max(launches, 1), 4), "iters_per_launch": iters,
+            "roofline": {"kernel": "k_chain_run (grid = %d chains)" % C, "bound": "hbm",
+                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "algorithmic_bytes_per_launch": round(nbytes / max(launches, 1), 1)}}
 
 
 def full_evaluate(tt, ctx, model, N, reps=50):

@@ -176,6 +176,12 @@ int td_chain_create(td_chain **out, td_ctx *ctx, const td_chain_params *params, 
 int td_chain_destroy(td_chain *ch);
 /* Run `iterations` proposals (TD_inversion_function.jl:70-274 loop body). */
 int td_chain_run(td_chain *ch, int64_t iterations);
+/* Run `iterations` proposals on each of `nchains` chains of ONE context in a
+ * single launch, one workgroup per chain (independent chains / tempering
+ * replicas sharing a GPU: main_inversion.jl:15 pmap over chains).  Device
+ * engine: one kernel; host engine: the chains run one after the other.  Each
+ * chain's result is identical to td_chain_run(chain, iterations). */
+int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterations);
 int td_chain_stats_get(const td_chain *ch, td_chain_stats *st);
 /* Copy the current model out (cells arrays capacity `cap`; *nCells receives
  * the count; ptS_out[n] nullable). */

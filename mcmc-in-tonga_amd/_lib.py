@@ -63,6 +63,7 @@ SIGNATURES = {
                                        _i64]),
     "td_chain_destroy": (ctypes.c_int, [_vp]),
     "td_chain_run": (ctypes.c_int, [_vp, _i64]),
+    "td_chain_run_batch": (ctypes.c_int, [ctypes.POINTER(_vp), _i64, _i64]),
     "td_chain_stats_get": (ctypes.c_int, [_vp, ctypes.POINTER(TdChainStats)]),
     "td_chain_get_model": (ctypes.c_int, [_vp, _pd, _pd, _pd, _pd, _i64, _pi64, _pd, _pd]),
     "td_chain_set_temperature": (ctypes.c_int, [_vp, _d]),

@@ -101,6 +101,17 @@ class Chain:
         check(lib().td_chain_set_temperature(self.h, float(T)), self.ctx.h)
 
 
+def run_batch(chains, iterations):
+    """``iterations`` proposals on every chain of one context in ONE launch
+    (one workgroup per chain, td_chain_run_batch) -- several independent
+    chains or tempering replicas per GPU."""
+    chains = list(chains)
+    if not chains:
+        return
+    arr = (ctypes.c_void_p * len(chains))(*[c.h for c in chains])
+    check(lib().td_chain_run_batch(arr, len(chains), int(iterations)), chains[0].ctx.h)
+
+
 def build_starting(TD_parameters, dataStruct, seed=1, chain=1):
     """MCsub.jl:76-121 (log-uniform nCells, uniform cells, zeta ~ U(0, zeta_scale)),
     drawn by the chain's RNG; returns (model, dataStruct, valid)."""

@@ -30,11 +30,6 @@ int hip_err(td_ctx *ctx, hipError_t e, const char *what) {
     return set_err(ctx, TD_ERR_HIP, m);
 }
 
-#define TD_HIP(ctx, call)                                 \
-    do {                                                  \
-        hipError_t e_ = (call);                           \
-        if (e_ != hipSuccess) return hip_err(ctx, e_, #call); \
-    } while (0)
 
 // Julia 1.5 Base.sum(::Vector{Float64}) association: n < 16 sequential;
 // otherwise pairwise over 1024-blocks, each block v=a1+a2 then 4 x 8-lane
@@ -133,10 +128,10 @@ void free_ctx(td_ctx *c) {
     c->timer.release();
     void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->cells,
                    c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->ptS, c->phi,
-                   c->q, c->q_i, c->q_z};
+                   c->q, c->q_i, c->q_z, c->chain_desc};
     for (void *p : dev)
         if (p) (void)hipFree(p);
-    void *host[] = {c->h_cells, c->h_out, c->h_best_i, c->h_q, c->h_q_i, c->h_q_z};
+    void *host[] = {c->h_cells, c->h_out, c->h_best_i, c->h_q, c->h_q_i, c->h_q_z, c->h_chain_desc};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -433,13 +433,63 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
     hipEvent_t t0 = tm ? tm->begin(ch->ctx->stream) : nullptr;
     e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, ch->ctx->stream);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "chain descriptor upload");
-    e = chain_run(ch->dev, ch->dev_ptr, iterations, ch->ctx->stream);
+    e = chain_run(&ch->dev, ch->dev_ptr, 1, iterations, ch->ctx->stream);
     if (tm) tm->end("chain_run", t0, ch->ctx->stream);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "k_chain_run launch");
     const int64_t before = ch->stats.iterations;
     int rc = device_pull_scalars(ch);
     ch->stats.iterations = before + iterations;
     return rc;
+}
+
+int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterations) {
+    if (!chains || nchains <= 0 || iterations < 0 || nchains > INT32_MAX) return TD_ERR_ARG;
+    td_ctx *c = chains[0] ? chains[0]->ctx : nullptr;
+    if (!c) return TD_ERR_ARG;
+    bool host = false;
+    for (int64_t b = 0; b < nchains; ++b) {
+        if (!chains[b] || chains[b]->ctx != c)
+            return set_err(c, TD_ERR_ARG, "td_chain_run_batch: every chain must be non-NULL and share one context");
+        host |= chains[b]->engine == TD_ENGINE_HOST;
+        for (int64_t k = 0; k < b; ++k)
+            if (chains[k] == chains[b]) return set_err(c, TD_ERR_ARG, "td_chain_run_batch: a chain appears twice");
+    }
+    if (iterations == 0) return TD_OK;
+    if (host || nchains == 1) {  // the host engine is the sequential parity twin
+        for (int64_t b = 0; b < nchains; ++b) {
+            int rc = td_chain_run(chains[b], iterations);
+            if (rc) return rc;
+        }
+        return TD_OK;
+    }
+    TD_HIP(c, hipSetDevice(c->device));
+    const size_t bytes = sizeof(DevChain) * (size_t)nchains;
+    if (bytes > c->chain_desc_bytes) {
+        TD_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->chain_desc) (void)hipFree(c->chain_desc);
+        if (c->h_chain_desc) (void)hipHostFree(c->h_chain_desc);
+        c->chain_desc = c->h_chain_desc = nullptr;
+        c->chain_desc_bytes = 0;
+        TD_HIP(c, hipMalloc(&c->chain_desc, bytes));
+        TD_HIP(c, hipHostMalloc(&c->h_chain_desc, bytes, hipHostMallocDefault));
+        c->chain_desc_bytes = bytes;
+    }
+    TD_HIP(c, hipStreamSynchronize(c->stream));  // the pinned staging may still feed a previous copy
+    DevChain *hd = static_cast<DevChain *>(c->h_chain_desc);
+    for (int64_t b = 0; b < nchains; ++b) hd[b] = chains[b]->dev;
+    Timer *tm = c->timer.on ? &c->timer : nullptr;
+    hipEvent_t t0 = tm ? tm->begin(c->stream) : nullptr;
+    TD_HIP(c, hipMemcpyAsync(c->chain_desc, hd, bytes, hipMemcpyHostToDevice, c->stream));
+    hipError_t e = chain_run(hd, static_cast<const DevChain *>(c->chain_desc), (int)nchains, iterations, c->stream);
+    if (tm) tm->end("chain_run", t0, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (batch)");
+    for (int64_t b = 0; b < nchains; ++b) {
+        const int64_t before = chains[b]->stats.iterations;
+        int rc = device_pull_scalars(chains[b]);
+        chains[b]->stats.iterations = before + iterations;
+        if (rc) return rc;
+    }
+    return TD_OK;
 }
 
 int td_chain_stats_get(const td_chain *ch, td_chain_stats *st) {

@@ -108,8 +108,9 @@ struct DevChain {
 // Build the cache from scratch for the cells currently in slots 0..ncells-1
 // (order = rank = identity): nearest search, ray sums, chi^2 prefix, tile maxima.
 hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, hipStream_t s);
-// Run `iters` iterations inside one persistent workgroup.
-// `dptr` = device copy of `d` (the kernel reads its fields from global memory).
-hipError_t chain_run(const DevChain &d, const DevChain *dptr, int64_t iters, hipStream_t s);
+// Run `iters` iterations of `nchains` chains, one persistent workgroup each
+// (workgroup b runs chain b).  `host` = the descriptors, `dev` = their device
+// copy, contiguous (the kernel reads its fields from global memory).
+hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s);
 
 }  // namespace tdstar

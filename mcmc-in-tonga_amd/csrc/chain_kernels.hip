@@ -28,6 +28,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 
 #include "chain_dev.h"
@@ -396,7 +397,7 @@ __device__ __forceinline__ double tile_lb2(const float *lo, const float *hi, int
 
 template <bool SMALL>
 __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters) {
-    const DevChain &d = *dptr;  // fields read from memory as needed, not pinned in registers
+    const DevChain &d = dptr[blockIdx.x];  // fields read from memory as needed, not pinned in registers
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Shared &sh = *reinterpret_cast<Shared *>(lds);
     const LdsPlan L = lds_plan(d.ntiles, d.n, d.cap, SMALL);
@@ -847,16 +848,22 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
     return e;
 }
 
-hipError_t chain_run(const DevChain &d, const DevChain *dptr, int64_t iters, hipStream_t s) {
-    const LdsPlan small = lds_plan(d.ntiles, d.n, d.cap, true);
-    if (small.total <= kLdsBudget) {
+hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s) {
+    // one LDS size for the whole grid: the largest plan of any chain; the
+    // small (LDS-mirrored) variant only if every chain fits
+    size_t small = 0, big = 0;
+    for (int b = 0; b < nchains; ++b) {
+        const DevChain &d = host[b];
+        small = std::max(small, lds_plan(d.ntiles, d.n, d.cap, true).total);
+        big = std::max(big, lds_plan(d.ntiles, d.n, d.cap, false).total);
+    }
+    if (small <= kLdsBudget) {
         hipError_t e = hipFuncSetAttribute((const void *)k_chain_run<true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)small.total);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)small);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_chain_run<true>, dim3(1), dim3(kChainThreads), small.total, s, dptr, (long long)iters);
+        hipLaunchKernelGGL(k_chain_run<true>, dim3(nchains), dim3(kChainThreads), small, s, dev, (long long)iters);
     } else {
-        const size_t lds = lds_plan(d.ntiles, d.n, d.cap, false).total;
-        hipLaunchKernelGGL(k_chain_run<false>, dim3(1), dim3(kChainThreads), lds, s, dptr, (long long)iters);
+        hipLaunchKernelGGL(k_chain_run<false>, dim3(nchains), dim3(kChainThreads), big, s, dev, (long long)iters);
     }
     return hipGetLastError();
 }

@@ -44,6 +44,9 @@ struct td_ctx {
     double *h_q_z = nullptr;
 
     tdstar::Timer timer;                // per-kernel HIP-event timing (td_timing_*)
+    void *chain_desc = nullptr;         // device array of chain descriptors (td_chain_run_batch)
+    size_t chain_desc_bytes = 0;
+    void *h_chain_desc = nullptr;       // pinned staging of the same
     std::string err;
 };
 
@@ -52,6 +55,13 @@ namespace tdstar {
 // Error helpers shared by api.cpp / chain.cpp.
 int set_err(td_ctx *ctx, int code, const std::string &msg);
 int hip_err(td_ctx *ctx, hipError_t e, const char *what);
+
+// Return the status of a failing HIP call (message names the call).
+#define TD_HIP(ctx, call)                                 \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hip_err(ctx, e_, #call); \
+    } while (0)
 // Make room for `ncells` cells (device + pinned staging).
 int ensure_cells(td_ctx *ctx, int64_t ncells);
 // Pack cells into the pinned staging buffer and upload them (async on ctx->stream).

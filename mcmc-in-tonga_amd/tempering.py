@@ -1,0 +1,149 @@
+"""Parallel tempering across chains -- the one exchange step of
+the multi-GPU path.
+
+The reference runs independent chains (``pmap`` over ``1:n_chains``,
+main_inversion.jl:15); each targets exp(-phi/2) times the prior
+(TD_inversion_function.jl:95-268).  A tempered replica at temperature T
+targets exp(-phi/(2T)) (``td_chain_params.temperature``).  Every ``K``
+proposals the replicas exchange temperatures -- never models:
+
+  1. every rank contributes (phi, level) of each local replica;
+     ``allgather`` over torch.distributed (RCCL over xGMI on the GPU box,
+     gloo in the CPU tests) -- 16 B per replica, latency-bound;
+  2. every rank decides the SAME swaps from the gathered vector: in round r
+     the adjacent level pairs (l, l+1) with l = r mod 2 are tried with
+     u ~ U(0,1) from a Philox stream keyed by (seed, r, l) and accepted when
+     log u < (phi_a - phi_b) * (1/(2 T_a) - 1/(2 T_b)) (a at level l, b at
+     level l+1: detailed balance for pi_T(m) ~ exp(-phi(m) / (2T)));
+  3. each rank sets the new temperature of its replicas
+     (``td_chain_set_temperature``) and continues.
+
+Replicas = ranks x chains per rank, so one GPU may hold several (global
+replica id g = rank * local + j).  The decision is a pure function of the
+gathered vector, the round and the seed (``decide_swaps``), so it is tested
+without any GPU (tests/test_tempering.py)."""
+import math
+
+import numpy as np
+
+
+def geometric_ladder(nrep, tmax=8.0):
+    """T_l = tmax ** (l / (nrep - 1)), l = 0..nrep-1 (T_0 = 1: the posterior)."""
+    if nrep <= 1:
+        return np.ones(max(nrep, 1))
+    return np.array([float(tmax) ** (l / (nrep - 1)) for l in range(nrep)])
+
+
+def _uniform(seed, rnd, level):
+    g = np.random.Generator(np.random.Philox(key=int(seed) & 0xFFFFFFFFFFFFFFFF, counter=[int(rnd), int(level), 0, 0]))
+    return float(g.random())
+
+
+def swap_log_alpha(phi_a, phi_b, t_a, t_b):
+    return (phi_a - phi_b) * (1.0 / (2.0 * t_a) - 1.0 / (2.0 * t_b))
+
+
+def decide_swaps(phis, levels, temps, rnd, seed):
+    """New level of every replica after round ``rnd``.
+
+    phis[g], levels[g]: gathered over all replicas; temps[l]: the ladder.
+    Returns (new_levels, tried, accepted) -- tried/accepted per level pair l
+    (index l = pair (l, l+1))."""
+    levels = np.asarray(levels, dtype=np.int64).copy()
+    R = len(levels)
+    owner = np.empty(R, dtype=np.int64)
+    owner[levels] = np.arange(R)  # replica currently at each level
+    tried = np.zeros(max(R - 1, 0), dtype=np.int64)
+    acc = np.zeros(max(R - 1, 0), dtype=np.int64)
+    for l in range(int(rnd) % 2, R - 1, 2):
+        a, b = owner[l], owner[l + 1]
+        tried[l] += 1
+        la = swap_log_alpha(phis[a], phis[b], temps[l], temps[l + 1])
+        u = _uniform(seed, rnd, l)
+        if la >= 0.0 or (u > 0.0 and math.log(u) < la):
+            levels[a], levels[b] = l + 1, l
+            owner[l], owner[l + 1] = b, a
+            acc[l] += 1
+    return levels, tried, acc
+
+
+class Exchange:
+    """allgather of a small float64 vector per rank (torch.distributed).
+    ``device`` = the torch device tensors live on for the backend (cuda for
+    nccl/RCCL, cpu for gloo).  Single process: identity."""
+
+    def __init__(self, dist=None, device="cpu"):
+        self.dist = dist
+        self.device = device
+        self.world = dist.get_world_size() if dist is not None else 1
+        self.rank = dist.get_rank() if dist is not None else 0
+
+    def allgather(self, vec):
+        vec = np.ascontiguousarray(vec, dtype=np.float64)
+        if self.dist is None or self.world == 1:
+            return vec.copy()
+        import torch
+
+        t = torch.from_numpy(vec).to(self.device)
+        out = torch.empty(self.world * t.numel(), dtype=torch.float64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t)
+        return out.cpu().numpy()
+
+
+class TemperingLadder:
+    """Parallel tempering over ``chains`` (this rank's replicas) and the
+    other ranks' replicas.  Chains need ``run(k)``, ``stats()['phi']`` and
+    ``set_temperature(T)`` (``chain.Chain`` or any stand-in)."""
+
+    def __init__(self, chains, exchange=None, tmax=8.0, seed=12345):
+        self.chains = list(chains)
+        self.ex = exchange or Exchange()
+        self.local = len(self.chains)
+        self.R = self.ex.world * self.local
+        self.temps = geometric_ladder(self.R, tmax)
+        self.seed = seed
+        self.rnd = 0
+        # replica g starts at level g
+        self.levels = np.arange(self.R, dtype=np.int64)
+        self.tried = np.zeros(max(self.R - 1, 0), dtype=np.int64)
+        self.accepted = np.zeros(max(self.R - 1, 0), dtype=np.int64)
+        for j, ch in enumerate(self.chains):
+            ch.set_temperature(float(self.temps[self.gid(j)]))
+        # td_chain replicas of one context run in one launch, one workgroup each
+        self.batch = self.local > 1 and all(hasattr(c, "h") and getattr(c, "ctx", None) is self.chains[0].ctx
+                                            for c in self.chains)
+
+    def gid(self, j):
+        return self.ex.rank * self.local + j
+
+    def step(self, k):
+        """k proposals on every local replica, then one swap round."""
+        if self.batch:
+            from .chain import run_batch
+
+            run_batch(self.chains, k)  # all local replicas in one launch
+        else:
+            for ch in self.chains:
+                ch.run(k)
+        mine = np.array([ch.stats()["phi"] for ch in self.chains], dtype=np.float64)
+        allphi = self.ex.allgather(mine)
+        new, tried, acc = decide_swaps(allphi, self.levels, self.temps, self.rnd, self.seed)
+        self.tried += tried
+        self.accepted += acc
+        for j, ch in enumerate(self.chains):
+            g = self.gid(j)
+            if new[g] != self.levels[g]:
+                ch.set_temperature(float(self.temps[new[g]]))
+        self.levels = new
+        self.rnd += 1
+        return allphi
+
+    def cold_local(self):
+        """Index of the local chain at T = 1, or None (another rank holds it)."""
+        for j in range(self.local):
+            if self.levels[self.gid(j)] == 0:
+                return j
+        return None
+
+    def swap_rates(self):
+        return [float(a) / t if t else 0.0 for a, t in zip(self.accepted, self.tried)]

@@ -120,3 +120,37 @@ def test_clustered_and_boundary_cells(tt, ds, ctx):
         host.run(200)
         assert dev.stats()["phi"] == host.stats()["phi"]
     assert same_models(dev.model(), host.model())
+
+
+def test_tempering_ladder_device_matches_host(tt, ds, ctx):
+    """Three tempered replicas on one GPU exchanging temperatures every 50
+    proposals: the device chains make exactly the host chains' moves and swaps."""
+    prm = tt.define_TDstructrure().replace(max_cells=300)
+    runs = {}
+    for eng in (tt.TD_ENGINE_DEVICE, tt.TD_ENGINE_HOST):
+        chains = [make(tt, ctx, prm, tt.random_model(150 + 20 * j, 30 + j), 30 + j, eng, chain=1 + j)
+                  for j in range(3)]
+        lad = tt.TemperingLadder(chains, tmax=8.0, seed=77)
+        trace = [list(lad.step(50)) + list(lad.levels) for _ in range(8)]
+        runs[eng] = (trace, [c.model() for c in chains], lad.swap_rates())
+    assert runs[tt.TD_ENGINE_DEVICE][0] == runs[tt.TD_ENGINE_HOST][0]
+    for a, b in zip(runs[tt.TD_ENGINE_DEVICE][1], runs[tt.TD_ENGINE_HOST][1]):
+        assert same_models(a, b)
+
+
+def test_batched_chains_equal_single_launches(tt, ds, ctx):
+    """td_chain_run_batch (one workgroup per chain, one launch) gives every
+    chain exactly what td_chain_run gives it alone."""
+    prm = tt.define_TDstructrure().replace(max_cells=700)
+    specs = [(60, 41), (300, 42), (600, 43), (150, 44), (8, 45)]
+    solo = []
+    for ncell, seed in specs:
+        c = make(tt, ctx, prm, tt.random_model(ncell, seed), seed, tt.TD_ENGINE_DEVICE, chain=seed)
+        c.run(400)
+        solo.append((c.stats(), c.model()))
+    batch = [make(tt, ctx, prm, tt.random_model(n, s), s, tt.TD_ENGINE_DEVICE, chain=s) for n, s in specs]
+    tt.run_batch(batch, 150)
+    tt.run_batch(batch, 250)
+    for c, (st, m) in zip(batch, solo):
+        assert c.stats()["phi"] == st["phi"] and c.stats()["accepted"] == st["accepted"]
+        assert same_models(c.model(), m)

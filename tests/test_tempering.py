@@ -1,0 +1,130 @@
+"""Parallel-tempering exchange: swap decisions, the allgather
+over torch.distributed (gloo, world_size 2, CPU), and that a tempered ladder
+of toy chains still samples the right cold distribution.  The GPU chains use
+the same TemperingLadder (tests/test_gpu_chain.py::test_tempering_ladder_*)."""
+import json
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import tonga
+
+tt = tonga.load()
+from mcmc_in_tonga_amd import tempering  # noqa: E402
+
+
+class ToyChain:
+    """1-D Metropolis chain with phi(x) = x^2: targets exp(-x^2 / (2T)) = N(0, T)."""
+
+    def __init__(self, seed):
+        self.rng = np.random.default_rng(seed)
+        self.x = 3.0
+        self.T = 1.0
+        self.samples = []
+
+    def set_temperature(self, T):
+        self.T = T
+
+    def run(self, k):
+        for _ in range(k):
+            xn = self.x + self.rng.normal() * 1.5
+            d = (xn * xn - self.x * self.x) / (2 * self.T)
+            if d <= 0 or math.log(self.rng.random()) < -d:
+                self.x = xn
+
+    def stats(self):
+        return {"phi": self.x * self.x}
+
+
+def test_ladder_is_geometric():
+    t = tempering.geometric_ladder(4, 8.0)
+    assert t[0] == 1.0 and abs(t[-1] - 8.0) < 1e-12
+    assert np.allclose(t[1:] / t[:-1], 2.0)
+    assert list(tempering.geometric_ladder(1)) == [1.0]
+
+
+def test_swap_rule():
+    temps = tempering.geometric_ladder(4, 8.0)
+    # a hotter replica with a lower misfit always moves down (log alpha > 0)
+    lv, tried, acc = tempering.decide_swaps([100.0, 10.0, 5.0, 1.0], [0, 1, 2, 3], temps, rnd=0, seed=1)
+    assert list(lv) == [1, 0, 3, 2] and list(tried) == [1, 0, 1] and list(acc) == [1, 0, 1]
+    # odd rounds try the (1,2) pair only
+    lv, tried, _ = tempering.decide_swaps([1.0, 5.0, 10.0, 100.0], [0, 1, 2, 3], temps, rnd=1, seed=1)
+    assert list(tried) == [0, 1, 0]
+    # log alpha = (phi_a - phi_b)(1/2T_a - 1/2T_b)
+    assert tempering.swap_log_alpha(3.0, 1.0, 1.0, 2.0) == pytest.approx(2.0 * (0.5 - 0.25))
+    # always a permutation, deterministic in (round, seed)
+    rng = np.random.default_rng(0)
+    lv = np.arange(6)
+    for r in range(50):
+        phis = rng.uniform(0, 50, 6)
+        a, _, _ = tempering.decide_swaps(phis, lv, tempering.geometric_ladder(6), r, 7)
+        b, _, _ = tempering.decide_swaps(phis, lv, tempering.geometric_ladder(6), r, 7)
+        assert np.array_equal(a, b) and sorted(a) == list(range(6))
+        lv = a
+
+
+def test_swap_acceptance_frequency():
+    temps = np.array([1.0, 2.0])
+    la = tempering.swap_log_alpha(1.0, 3.0, 1.0, 2.0)  # = -0.5
+    hits = sum(tempering.decide_swaps([1.0, 3.0], [0, 1], temps, r, 3)[2][0] for r in range(0, 8000, 2))
+    assert abs(hits / 4000 - math.exp(la)) < 0.03
+
+
+def test_cold_replica_samples_posterior():
+    chains = [ToyChain(s) for s in range(4)]
+    lad = tempering.TemperingLadder(chains, tmax=16.0, seed=5)
+    cold = []
+    for r in range(6000):
+        lad.step(2)
+        j = lad.cold_local()
+        cold.append(chains[j].x)
+    cold = np.array(cold[500:])
+    assert abs(np.mean(cold)) < 0.15
+    assert abs(np.var(cold) - 1.0) < 0.15  # N(0, T=1)
+    assert all(0.05 < r < 0.95 for r in lad.swap_rates())
+
+
+def _worker(rank, world, port, outdir, rounds):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    chains = [ToyChain(100 + rank * 2 + j) for j in range(2)]
+    lad = tempering.TemperingLadder(chains, tempering.Exchange(dist, "cpu"), tmax=8.0, seed=9)
+    trace = []
+    for _ in range(rounds):
+        phis = lad.step(3)
+        trace.append([list(map(float, phis)), list(map(int, lad.levels))])
+    with open(os.path.join(outdir, "r%d.json" % rank), "w") as f:
+        json.dump({"trace": trace, "temps": [c.T for c in chains]}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_gloo_world2_matches_single_process(tmp_path):
+    import torch.multiprocessing as mp
+
+    rounds = 40
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), rounds), nprocs=2, join=True)
+    r0 = json.load(open(tmp_path / "r0.json"))
+    r1 = json.load(open(tmp_path / "r1.json"))
+    assert r0["trace"] == r1["trace"]  # every rank saw the same gather and made the same swaps
+    # the same 4 replicas in one process (replica g = rank*2 + j, same seeds)
+    chains = [ToyChain(100 + g) for g in range(4)]
+    lad = tempering.TemperingLadder(chains, tmax=8.0, seed=9)
+    for k in range(rounds):
+        phis = lad.step(3)
+        assert list(map(float, phis)) == r0["trace"][k][0]
+        assert list(map(int, lad.levels)) == r0["trace"][k][1]
+    assert [c.T for c in chains] == r0["temps"] + r1["temps"]
