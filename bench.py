@@ -43,6 +43,18 @@ FP64_VALU_PEAK_TFLOPS = 78.6   # FP64 vector, FMA counted as 2 (spec)
 FP64_NOFMA_PEAK_TFLOPS = FP64_VALU_PEAK_TFLOPS / 2
 
 
+def measured_traffic(key):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes of this
+    same command (profiles/traffic.json, written from tools/profile.sh
+    output: FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            t = json.load(f)[key]
+        return round(float(t["traffic_bytes_per_launch"]), 1), t["source"]
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -176,10 +188,13 @@ def main():
                        "rate": round(sum(acc) / max(sum(prop), 1), 4)},
         "roofline": {"kernel": "k_chain_run", "bound": "hbm", "achieved": round(achieved, 3),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": None, "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
+                     "traffic": None, "traffic_source": None,
+                     "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
                      "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
                      "note": "one persistent workgroup per chain: latency-bound by design (see DESIGN.md)"},
     }
+    if C == 1 and ladder is None and N == 5000 and a.iters_per_step == 5000:
+        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = measured_traffic("k_chain_run/single")
     if ladder is not None:
         out["tempering"] = {"replicas": ladder.R, "temps": [round(t, 4) for t in ladder.temps],
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
@@ -217,13 +232,16 @@ def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3):
     for c in chains:
         c.close()
     value = C * iters * steps / el
+    tr, src = measured_traffic("k_chain_run/many256")
     achieved = nbytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
     return {"chains": C, "proposals_per_s": round(value, 1), "per_chain_proposals_per_s": round(value / C, 1),
             "ms_per_launch": round(kms / max(launches, 1), 4), "iters_per_launch": iters,
             "roofline": {"kernel": "k_chain_run (grid = %d chains)" % C, "bound": "hbm",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "algorithmic_bytes_per_launch": round(nbytes / max(launches, 1), 1)}}
+                         "algorithmic_bytes_per_launch": round(nbytes / max(launches, 1), 1),
+                         "traffic": tr if C == 256 and iters == 1000 else None,
+                         "traffic_source": src if C == 256 and iters == 1000 else None}}
 
 
 def full_evaluate(tt, ctx, model, N, reps=50):

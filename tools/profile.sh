@@ -1,0 +1,18 @@
+#!/bin/bash
+# rocprofv3 evidence for profiles/: kernel trace + stats, then one PMC pass per
+# counter group (never combined with any trace domain).  usage: tools/profile.sh TAG
+set -o pipefail
+TAG=${1:-prof}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+run() {  # name, bench args...
+    local name=$1; shift
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name/trace -o run -- python3 bench.py "$@" > $OUT/$name/trace.log 2>&1 || return 1
+    timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$name/fetch -o run -- python3 bench.py "$@" > $OUT/$name/fetch.log 2>&1 || return 1
+    timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$name/write -o run -- python3 bench.py "$@" > $OUT/$name/write.log 2>&1 || return 1
+    timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/$name/sq -o run -- python3 bench.py "$@" > $OUT/$name/sq.log 2>&1 || return 1
+}
+mkdir -p $OUT/single $OUT/many
+run single --steps 3 --warmup 1 --no-cpu-baseline --batch-chains 0 && \
+run many --steps 2 --warmup 1 --no-cpu-baseline --no-full-evaluate --batch-chains 0 --chains-per-gpu 256 --iters-per-step 1000
