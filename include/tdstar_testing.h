@@ -29,9 +29,11 @@ void tdt_draws(uint64_t seed, uint32_t chain, uint64_t iter, double out[7]);
 int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const double *cx, const double *cy,
                 const double *cz, const double *czeta, double czeta_birth, double out[8]);
 /* Diagnostic: turn the DEVICE engine's per-phase s_memtime stamps on/off and
- * read the accumulated shader cycles per phase (0 draw, 1 birth/death query,
- * 2 tiles, 3 points, 4 orphans, 5 ray marks, 6 ray sums, 7 chi^2, 8 accept,
- * 9 commit).  Never enabled in measured runs. */
+ * read the accumulated shader cycles: [0..6] phases A..G of k_chain_run
+ * (draw, tiles + birth/death query, points, orphans, ray sums, chi^2 +
+ * accept, commit), [8..11] whole proposals by action (birth, death, change,
+ * move), [15] grid searches that fell back to a full scan.  Never enabled in
+ * measured runs. */
 int tdt_chain_profile(td_chain *ch, int enable, int64_t out[16]);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,

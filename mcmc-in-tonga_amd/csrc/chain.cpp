@@ -168,11 +168,14 @@ int device_setup(td_chain *ch) {
     const int64_t P = c->g.P, n = c->g.n;
     // ---- tiles: <= kTilePts consecutive points of one ray; bounding boxes
     //      rounded OUTWARD to FP32 (the lower bound stays valid, LDS holds them) ----
-    std::vector<int> tstart, tile_of((size_t)P), pt_ray((size_t)P);
+    std::vector<int> tstart, tray, pt_ray((size_t)P);
     for (int64_t r = 0; r < n; ++r) {
         const int a = c->ray_off_host[(size_t)r], b = c->ray_off_host[(size_t)r + 1];
         for (int q = a; q < b; ++q) pt_ray[(size_t)q] = (int)r;
-        for (int q = a; q < b; q += kTilePts) tstart.push_back(q);
+        for (int q = a; q < b; q += kTilePts) {
+            tstart.push_back(q);
+            tray.push_back((int)r);
+        }
     }
     const int ntiles = (int)tstart.size();
     tstart.push_back((int)P);
@@ -180,7 +183,6 @@ int device_setup(td_chain *ch) {
     for (int t = 0; t < ntiles; ++t) {
         double l[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, h[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
         for (int q = tstart[(size_t)t]; q < tstart[(size_t)t + 1]; ++q) {
-            tile_of[(size_t)q] = t;
             const double v[3] = {c->hx[(size_t)q], c->hy[(size_t)q], c->hz[(size_t)q]};
             for (int a = 0; a < 3; ++a)
                 if (!std::isnan(v[a])) {
@@ -226,7 +228,7 @@ int device_setup(td_chain *ch) {
     size_t bytes = 0;
     auto add = [&](size_t b) { bytes += ((b + 255) / 256) * 256; };
     const size_t Pn = (size_t)std::max<int64_t>(P, 1), nn = (size_t)std::max<int64_t>(n, 1);
-    add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * Pn); add(sizeof(int) * Pn);
+    add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * Pn);
     add(sizeof(float) * 3 * ntiles); add(sizeof(float) * 3 * ntiles); add(sizeof(double) * (ntiles + 1));
     add(sizeof(double) * 4 * cap); for (int i = 0; i < 4; ++i) add(sizeof(int) * cap);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn);
@@ -247,11 +249,11 @@ int device_setup(td_chain *ch) {
     d.P = (int)P;
     d.n = (int)n;
     int *tile_start = carve<int>(cur, ntiles + 1);
-    int *tile_of_d = carve<int>(cur, Pn);
+    int *tile_ray_d = carve<int>(cur, ntiles + 1);
     int *pt_ray_d = carve<int>(cur, Pn);
     float *tlo = carve<float>(cur, 3 * (size_t)ntiles);
     float *thi = carve<float>(cur, 3 * (size_t)ntiles);
-    d.tile_start = tile_start; d.pt_ray = pt_ray_d; d.tile_lo = tlo; d.tile_hi = thi;
+    d.tile_start = tile_start; d.tile_ray = tile_ray_d; d.pt_ray = pt_ray_d; d.tile_lo = tlo; d.tile_hi = thi;
     d.tile_maxd = carve<double>(cur, ntiles + 1);
     d.ntiles = ntiles;
     double *cells = carve<double>(cur, 4 * (size_t)cap);
@@ -297,7 +299,7 @@ int device_setup(td_chain *ch) {
     s0.phi = 1.0;  // debug_prior: evaluate returns phi = 1 (MCsub.jl:131)
     struct Up { void *d; const void *h; size_t b; } ups[] = {
         {tile_start, tstart.data(), sizeof(int) * tstart.size()},
-        {tile_of_d, tile_of.data(), sizeof(int) * (size_t)P},
+        {tile_ray_d, tray.data(), sizeof(int) * tray.size()},
         {pt_ray_d, pt_ray.data(), sizeof(int) * (size_t)P},
         {tlo, lo.data(), sizeof(float) * lo.size()},
         {thi, hi.data(), sizeof(float) * hi.size()},

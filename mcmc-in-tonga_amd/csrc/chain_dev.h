@@ -75,6 +75,7 @@ struct DevChain {
     int P, n;
     // tiles of <= kTilePts consecutive points of one ray
     const int *tile_start;            // [ntiles+1]
+    const int *tile_ray;              // [ntiles] ray of each tile
     const float *tile_lo, *tile_hi;   // [3][ntiles] SoA, outward-rounded to FP32
     double *tile_maxd;                // [ntiles] max cached distance of the tile's points
     int ntiles;

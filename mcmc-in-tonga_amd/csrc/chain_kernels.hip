@@ -42,8 +42,14 @@ namespace {
 using tdchain::Proposal;
 
 constexpr int kWaves = kChainThreads / 64;
-constexpr int kBatch = kWaves;  // query points searched together (one wave each)
-constexpr int kSub = 4;         // queries per full-scan pass (register budget)
+static_assert(kTilePts == 16, "a tile is one 16-lane DPP row (row_max_u64)");
+constexpr int kOrphanLds = 256; // orphan records kept in LDS (more: read back from HBM)
+
+// A point whose nearest cell is removed or moved: re-searched in phase D.
+struct OrphanRec {
+    double x, y, z;
+    int q, ray;
+};
 
 __device__ __forceinline__ double dist2(double cx, double cy, double cz, double x, double y, double z) {
     // (mx-x)^2 + (my-y)^2 + (mz-z)^2, MCsub.jl:254 -- same ops as k_nn_partial
@@ -60,22 +66,54 @@ __device__ __forceinline__ bool better(double d, int r, double bd, int br) {
     return d < bd || (d == bd && d < kSentinel && r < br);
 }
 
-__device__ __forceinline__ void wave_min_dr(double &dd, int &rr) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double od = __shfl_xor(dd, off, 64);
-        const int orr = __shfl_xor(rr, off, 64);
-        if (better(od, orr, dd, rr)) {
-            dd = od;
-            rr = orr;
-        }
-    }
+// ---- cross-lane reductions on 64-bit keys through DPP (VALU, no LDS) ----
+// A non-negative double orders like its bit pattern, so distances reduce as
+// unsigned 64-bit keys.  update_dpp returns `old` in lanes whose source is out
+// of the row or masked off, so `old` is the identity of the reduction.
+template <int CTRL, int RM>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v, unsigned long long idn) {
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)idn, (int)(unsigned)v, CTRL, RM, 0xf, false);
+    const int hi =
+        __builtin_amdgcn_update_dpp((int)(unsigned)(idn >> 32), (int)(unsigned)(v >> 32), CTRL, RM, 0xf, false);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+// min over the 64 lanes of the wave, returned to every lane
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+    constexpr unsigned long long I = ~0ull;
+    v = umin64(v, dpp_u64<0x111, 0xf>(v, I));  // row_shr:1
+    v = umin64(v, dpp_u64<0x112, 0xf>(v, I));  // row_shr:2
+    v = umin64(v, dpp_u64<0x114, 0xf>(v, I));  // row_shr:4
+    v = umin64(v, dpp_u64<0x118, 0xf>(v, I));  // row_shr:8  -> lane 15 of a row: row min
+    v = umin64(v, dpp_u64<0x142, 0xa>(v, I));  // row_bcast:15 into rows 1, 3
+    v = umin64(v, dpp_u64<0x143, 0xc>(v, I));  // row_bcast:31 into rows 2, 3 -> lane 63: min
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+// max over each row of 16 lanes, valid in the row's last lane (lane % 16 == 15)
+__device__ __forceinline__ unsigned long long row_max_u64(unsigned long long v) {
+    v = umax64(v, dpp_u64<0x111, 0xf>(v, 0ull));
+    v = umax64(v, dpp_u64<0x112, 0xf>(v, 0ull));
+    v = umax64(v, dpp_u64<0x114, 0xf>(v, 0ull));
+    v = umax64(v, dpp_u64<0x118, 0xf>(v, 0ull));
+    return v;
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 struct OverlayZeta {
     const unsigned char *flag;
     const double *cand, *cur;
-    __device__ __forceinline__ double operator()(int k) const { return flag[k] ? cand[k] : cur[k]; }
+    __device__ __forceinline__ double operator()(int k) const {
+        const double a = cand[k], b = cur[k];  // both loads issued at once, then select
+        return flag[k] ? a : b;
+    }
 };
 
 struct Shared {
@@ -89,18 +127,15 @@ struct Shared {
     int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site
     double g_ox, g_oy, g_oz, g_nx, g_ny, g_nz;
     // chain scalars, resident for the whole launch
-    long long iter, evaluations, bytes, grid_fallbacks;
+    long long iter, evaluations, bytes;
     long long proposed[5], accepted[5];
     double phi;
     int ncells, nslots, nfree;
-    // nearest-cell queries
-    double qx[kBatch], qy[kBatch], qz[kBatch];
-    double res_d[kBatch], res_z[kBatch];
-    int res_s[kBatch];
-    int any_full;
-    double red_d[kWaves][kSub];
-    int red_r[kWaves][kSub];
-    long long prof[16], t_last;  // diagnostic phase stamps
+    double q_zeta;         // result of the birth/death Interpolation query
+    int grid_fallbacks32;  // grid searches that needed the full scan
+    int grid_ovf;          // LDS copy of *d.grid_overflow
+    OrphanRec orph[kOrphanLds];
+    long long prof[16], t_last, t_iter;  // diagnostic phase stamps
 };
 
 // Diagnostic phase stamp (lane 0 of wave 0, right after a barrier): cycles
@@ -116,8 +151,8 @@ struct Shared {
 
 // LDS carve-up (host and device agree on it through this function).
 struct LdsPlan {
-    size_t scratch, chi, draws, tlo, thi, tmaxd, tstart, thit, rayoff, ptS, prefix, cptS, cprefix, tS, sig, rflag,
-        rhit, ord, total;
+    size_t scratch, chi, draws, tlo, thi, tmaxd, tstart, thit, tray, rayoff, ptS, prefix, cptS, cprefix, tS, sig,
+        rflag, rhit, ord, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -134,6 +169,7 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
         L.tmaxd = o; o += align16(sizeof(double) * ntiles);
         L.tstart = o; o += align16(sizeof(int) * (ntiles + 1));
         L.thit = o; o += align16(sizeof(int) * (ntiles + 1));
+        L.tray = o; o += align16(sizeof(int) * ntiles);
         L.rayoff = o; o += align16(sizeof(int) * (n + 1));
         L.ptS = o; o += align16(sizeof(double) * n);
         L.prefix = o; o += align16(sizeof(double) * n);
@@ -154,187 +190,168 @@ struct Views {
     const float *tlo, *thi;
     double *tmaxd, *ptS, *prefix, *cptS, *cprefix, *chi;
     const double *tS, *sig;
-    const int *tstart, *ray_off;
+    const int *tstart, *ray_off, *tray;
     int *thit, *rflag, *rhit, *ord;
 };
 
-// Exact nearest live cell by scanning every slot (lexicographic distance,
-// Julia position), kSub queries per pass.  Fallback of the grid search
-// (rare: kept out of line so it does not cost the hot loop registers).
-__device__ __attribute__((noinline)) void block_search(const DevChain &d, const Views &v, Shared &sh, int nq, int skip, int moved, double mx,
-                             double my, double mz) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int nslots = sh.nslots;
-    for (int q0 = 0; q0 < nq; q0 += kSub) {
-        double bd[kSub];
-        int br[kSub];
+// Result of one nearest-cell query, the same in every lane of the wave.
+struct Nearest {
+    double d, z;  // squared distance (1e9 sentinel if none) and the cell's value (0.0 if none)
+    int s;        // slot (-1 if none)
+    bool proven;
+};
+
+// Exact nearest live cell by scanning every slot, ONE wave: lexicographic
+// (distance, Julia position), which is what v_nearest's first-index rule
+// gives (MCsub.jl:250-258).  Fallback of the grid search (rare: out of line).
+__device__ __attribute__((noinline)) Nearest wave_full_scan(const int *__restrict__ rank, const int *ord,
+                                                           const double *__restrict__ cx,
+                                                           const double *__restrict__ cy,
+                                                           const double *__restrict__ cz,
+                                                           const double *__restrict__ czeta, int cap, int nslots,
+                                                           int lane, double x, double y, double z, int skip,
+                                                           int moved, double mx, double my, double mz) {
+    double bd = kSentinel;
+    int br = INT_MAX;
+    constexpr int kScanUnroll = 8;  // all loads of a round issued before any use
+    for (int s0 = lane; s0 < nslots; s0 += kScanUnroll * 64) {
+        int r[kScanUnroll];
+        double px[kScanUnroll], py[kScanUnroll], pz[kScanUnroll];
 #pragma unroll
-        for (int q = 0; q < kSub; ++q) {
-            bd[q] = kSentinel;
-            br[q] = INT_MAX;
-        }
-        constexpr int kScanUnroll = 8;  // all loads of a round issued before any use
-        for (int s0 = tid; s0 < nslots; s0 += kScanUnroll * kChainThreads) {
-            int r[kScanUnroll];
-            double x[kScanUnroll], y[kScanUnroll], z[kScanUnroll];
-#pragma unroll
-            for (int u = 0; u < kScanUnroll; ++u) {
-                // unconditional loads from a clamped slot, masked afterwards (a select
-                // on the LOAD would make hipcc branch and wait per element)
-                const int s = min(s0 + u * kChainThreads, d.cap - 1);
-                r[u] = d.rank[s];
-                x[u] = d.cx[s];
-                y[u] = d.cy[s];
-                z[u] = d.cz[s];
-            }
-#pragma unroll
-            for (int u = 0; u < kScanUnroll; ++u) {
-                const int s = s0 + u * kChainThreads;
-                if (s >= nslots || r[u] < 0 || s == skip) continue;  // free slot / killed cell
-                if (s == moved) {
-                    x[u] = mx;
-                    y[u] = my;
-                    z[u] = mz;
-                }
-#pragma unroll
-                for (int q = 0; q < kSub; ++q)
-                    if (q0 + q < nq) {
-                        const double dd = dist2(x[u], y[u], z[u], sh.qx[q0 + q], sh.qy[q0 + q], sh.qz[q0 + q]);
-                        if (better(dd, r[u], bd[q], br[q])) {
-                            bd[q] = dd;
-                            br[q] = r[u];
-                        }
-                    }
-            }
+        for (int u = 0; u < kScanUnroll; ++u) {
+            // unconditional loads from a clamped slot, masked afterwards
+            const int s = min(s0 + u * 64, cap - 1);
+            r[u] = rank[s];
+            px[u] = cx[s];
+            py[u] = cy[s];
+            pz[u] = cz[s];
         }
 #pragma unroll
-        for (int q = 0; q < kSub; ++q)
-            if (q0 + q < nq) {
-                wave_min_dr(bd[q], br[q]);
-                if (lane == 0) {
-                    sh.red_d[wv][q] = bd[q];
-                    sh.red_r[wv][q] = br[q];
-                }
+        for (int u = 0; u < kScanUnroll; ++u) {
+            const int s = s0 + u * 64;
+            if (s >= nslots || r[u] < 0 || s == skip) continue;  // free slot / killed cell
+            if (s == moved) {
+                px[u] = mx;
+                py[u] = my;
+                pz[u] = mz;
             }
-        __syncthreads();
-        if (tid < kSub && q0 + tid < nq) {
-            double b = sh.red_d[0][tid];
-            int r = sh.red_r[0][tid];
-            for (int w = 1; w < kWaves; ++w)
-                if (better(sh.red_d[w][tid], sh.red_r[w][tid], b, r)) {
-                    b = sh.red_d[w][tid];
-                    r = sh.red_r[w][tid];
-                }
-            const int s = r != INT_MAX ? v.ord[r] : -1;
-            sh.res_d[q0 + tid] = b;
-            sh.res_s[q0 + tid] = s;
-            sh.res_z[q0 + tid] = s >= 0 ? d.czeta[s] : 0.0;
+            const double dd = dist2(px[u], py[u], pz[u], x, y, z);
+            if (better(dd, r[u], bd, br)) {
+                bd = dd;
+                br = r[u];
+            }
         }
-        __syncthreads();
     }
+    // lexicographic min: the distance first, then the position among equals
+    const unsigned long long kd = wave_min_u64((unsigned long long)__double_as_longlong(bd));
+    const bool at_min = (unsigned long long)__double_as_longlong(bd) == kd;
+    const unsigned long long kr = wave_min_u64(at_min ? (unsigned long long)(unsigned)br : ~0ull);
+    Nearest res;
+    res.d = __longlong_as_double((long long)kd);
+    res.proven = true;
+    if (res.d < kSentinel && kr != ~0ull) {
+        res.s = ord[(int)kr];
+        res.z = czeta[res.s];
+    } else {
+        res.s = -1;
+        res.z = 0.0;
+    }
+    return res;
 }
 
-// Nearest live cell through the bucket grid: wave q handles query q.  Lanes
-// 0..53 cover the 3x3x3 buckets around the query, 8 entries per bucket
+// Nearest live cell through the bucket grid, ONE wave, no block barrier.
+// Lanes 0..53 cover the 3x3x3 buckets around the query, 8 entries per bucket
 // (entries hold the cell coordinates inline: ONE round of loads).  The answer
 // is proven when its distance is strictly below the squared distance to the
-// outer faces of the block (every cell outside lies beyond a face) and no
-// other entry ties it and no bucket holds more than 8 entries; else
-// sh.any_full is set.  `skip` = the killed slot; slot `moved` is taken at
-// (mx,my,mz) instead of its stored site.
-__device__ void grid_search(const DevChain &d, Shared &sh, int nq, int skip, int moved, double mx, double my,
-                            double mz) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// outer faces of the block (every cell outside lies beyond a face), no other
+// entry ties it and no bucket holds more than 8 entries.  `skip` = the killed
+// slot; slot `moved` is taken at (mx,my,mz) instead of its stored site.
+__device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf, int lane, double x, double y,
+                                                    double z, int skip, int moved, double mx, double my, double mz) {
     const CellGrid &G = d.grid;
-    if (tid == 0) sh.any_full = 0;
-    if (wv < nq) {
-        const double x = sh.qx[wv], y = sh.qy[wv], z = sh.qz[wv];
-        const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
-                  bk = grid_axis(z, G.z0, G.iz, G.gz);
-        const int nb = lane % 27, grp = lane / 27;
-        const int ii = bi + nb % 3 - 1, jj = bj + (nb / 3) % 3 - 1, kk = bk + nb / 9 - 1;
-        const bool inb = lane < 54 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
-        const int b = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
-        const int cnt = d.bucket_count[b];
-        BucketEntry e[4];
+    const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
+              bk = grid_axis(z, G.z0, G.iz, G.gz);
+    const int nb = lane % 27, grp = lane / 27;
+    const int ii = bi + nb % 3 - 1, jj = bj + (nb / 3) % 3 - 1, kk = bk + nb / 9 - 1;
+    const bool inb = lane < 54 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
+    const int b = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
+    const int cnt = d.bucket_count[b];
+    BucketEntry e[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) e[u] = d.buckets[b * kBucketCap + grp * 4 + u];
-        double bd = kSentinel;
-        int bs = -1;
-        bool tie = false, overfull = inb && cnt > 8;
+    for (int u = 0; u < 4; ++u) e[u] = d.buckets[b * kBucketCap + grp * 4 + u];
+    double bd = kSentinel;
+    int bs = -1;
+    bool tie = false;
+    const bool overfull = inb && cnt > 8;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const bool ok = inb && grp * 4 + u < cnt && e[u].slot != skip && e[u].slot != moved;
-            const double dd = dist2(e[u].x, e[u].y, e[u].z, x, y, z);
-            if (ok) {
-                if (dd < bd) {
-                    bd = dd;
-                    bs = e[u].slot;
-                    tie = false;
-                } else if (dd == bd && dd < kSentinel) {
-                    tie = true;
-                }
-            }
-        }
-        if (lane == 63 && moved >= 0) {  // the moved cell, at its proposed site
-            const double dd = dist2(mx, my, mz, x, y, z);
+    for (int u = 0; u < 4; ++u) {
+        const bool ok = inb && grp * 4 + u < cnt && e[u].slot != skip && e[u].slot != moved;
+        const double dd = dist2(e[u].x, e[u].y, e[u].z, x, y, z);
+        if (ok) {
             if (dd < bd) {
                 bd = dd;
-                bs = moved;
-            }
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double od = __shfl_xor(bd, off, 64);
-            const int os = __shfl_xor(bs, off, 64);
-            const bool ot = __shfl_xor((int)tie, off, 64) != 0;
-            if (od < bd) {
-                bd = od;
-                bs = os;
-                tie = ot;
-            } else if (od == bd && od < kSentinel && os != bs) {
+                bs = e[u].slot;
+                tie = false;
+            } else if (dd == bd && dd < kSentinel) {
                 tie = true;
-            } else if (od == bd) {
-                tie = tie || ot;
             }
-        }
-        const bool any_over = __ballot(overfull) != 0ull;
-        if (lane == 0) {
-            // squared distance to the nearest outer face of the searched block
-            double lb = __builtin_huge_val();
-            auto face = [&lb](double v, double v0, double inv, double h, int g) {
-                const int i = grid_axis(v, v0, inv, g);
-                if (i - 1 > 0) {
-                    const double gap = v - (v0 + (double)(i - 1) * h);
-                    lb = gap > 0.0 ? fmin(lb, gap * gap) : 0.0;
-                }
-                if (i + 1 < g - 1) {
-                    const double gap = (v0 + (double)(i + 2) * h) - v;
-                    lb = gap > 0.0 ? fmin(lb, gap * gap) : 0.0;
-                }
-            };
-            face(x, G.x0, G.ix, G.hx, G.gx);
-            face(y, G.y0, G.iy, G.hy, G.gy);
-            face(z, G.z0, G.iz, G.hz, G.gz);
-            // the relative margin covers the rounding of bucket indices vs faces
-            const bool proven = *d.grid_overflow == 0 && !tie && !any_over && bd < lb * (1.0 - 1e-9);
-            sh.res_d[wv] = bd;
-            sh.res_s[wv] = bd < kSentinel ? bs : -1;
-            sh.res_z[wv] = bd < kSentinel ? d.czeta[bs] : 0.0;
-            if (!proven) atomicOr(&sh.any_full, 1);
         }
     }
-    __syncthreads();
+    if (lane == 63 && moved >= 0) {  // the moved cell, at its proposed site
+        const double dd = dist2(mx, my, mz, x, y, z);
+        if (dd < bd) {
+            bd = dd;
+            bs = moved;
+            tie = false;
+        } else if (dd == bd && dd < kSentinel) {
+            tie = true;
+        }
+    }
+    const double bz = d.czeta[bs >= 0 ? bs : 0];  // issued now, used after the reduction
+    const unsigned long long key = (unsigned long long)__double_as_longlong(bd);
+    const unsigned long long kmin = wave_min_u64(key);
+    const unsigned long long who = __ballot(key == kmin);
+    const int win = __builtin_ctzll(who);
+    Nearest res;
+    res.d = __longlong_as_double((long long)kmin);
+    const bool found = res.d < kSentinel;
+    // distinct slots at the minimum (a slot sits in one lane only), or a tie inside the winner
+    const bool tied = found && (__popcll(who) > 1 || __builtin_amdgcn_readlane((int)tie, win) != 0);
+    const bool any_over = __ballot(overfull) != 0ull;
+    res.s = found ? __builtin_amdgcn_readlane(bs, win) : -1;
+    res.z = found ? readlane_f64(bz, win) : 0.0;
+    // squared distance to the nearest outer face of the searched block
+    double lb = __builtin_huge_val();
+    auto face = [&lb](double v, double v0, double inv, double h, int g) {
+        const int i = grid_axis(v, v0, inv, g);
+        if (i - 1 > 0) {
+            const double gap = v - (v0 + (double)(i - 1) * h);
+            lb = gap > 0.0 ? fmin(lb, gap * gap) : 0.0;
+        }
+        if (i + 1 < g - 1) {
+            const double gap = (v0 + (double)(i + 2) * h) - v;
+            lb = gap > 0.0 ? fmin(lb, gap * gap) : 0.0;
+        }
+    };
+    face(x, G.x0, G.ix, G.hx, G.gx);
+    face(y, G.y0, G.iy, G.hy, G.gy);
+    face(z, G.z0, G.iz, G.hz, G.gz);
+    // the relative margin covers the rounding of bucket indices vs faces
+    res.proven = !ovf && !tied && !any_over && res.d < lb * (1.0 - 1e-9);
+    return res;
 }
 
-// Nearest live cell for nq query points: grid first, full scan if unproven.
-__device__ void nearest_queries(const DevChain &d, const Views &v, Shared &sh, int nq, int skip, int moved,
-                                double mx, double my, double mz) {
-    grid_search(d, sh, nq, skip, moved, mx, my, mz);
-    if (sh.any_full) {
-        if (threadIdx.x == 0) sh.grid_fallbacks += 1;
-        block_search(d, v, sh, nq, skip, moved, mx, my, mz);
+// Nearest live cell for one query, one wave: grid first, full scan if unproven.
+__device__ __forceinline__ Nearest wave_nearest(const DevChain &d, const Views &v, Shared &sh, int lane, double x,
+                                                double y, double z, int skip, int moved, double mx, double my,
+                                                double mz) {
+    Nearest r = wave_grid_search(d, sh.grid_ovf != 0, lane, x, y, z, skip, moved, mx, my, mz);
+    if (!r.proven) {
+        if (lane == 0) atomicAdd(&sh.grid_fallbacks32, 1);
+        r = wave_full_scan(d.rank, v.ord, d.cx, d.cy, d.cz, d.czeta, d.cap, sh.nslots, lane, x, y, z, skip, moved,
+                           mx, my, mz);
     }
+    return r;
 }
 
 // Apply the pending bucket-grid update (one wave).
@@ -348,6 +365,7 @@ __device__ void grid_apply(const DevChain &d, Shared &sh, int lane) {
         if (lane == 0) {
             if (m == 0ull) {
                 *d.grid_overflow = 1;  // bookkeeping lost track: stop trusting the grid
+                sh.grid_ovf = 1;
             } else {
                 d.buckets[b * kBucketCap + __builtin_ctzll(m)] = d.buckets[b * kBucketCap + cnt - 1];
                 d.bucket_count[b] = cnt - 1;
@@ -362,18 +380,18 @@ __device__ void grid_apply(const DevChain &d, Shared &sh, int lane) {
             d.bucket_count[b] = cnt + 1;
         } else {
             *d.grid_overflow = 1;
+            sh.grid_ovf = 1;
         }
     }
 }
 
-__device__ __forceinline__ void mark(const DevChain &d, const Views &v, Shared &sh, int p, int s, double dd,
+__device__ __forceinline__ void mark(const DevChain &d, const Views &v, Shared &sh, int p, int r, int s, double dd,
                                      double z) {
     d.cand_s[p] = s;
     d.cand_d[p] = dd;
     d.cand_z[p] = z;
     d.cand_flag[p] = 1;
     d.changed[atomicAdd(&sh.n_changed, 1)] = p;
-    const int r = d.pt_ray[p];
     if (atomicExch(&v.rflag[r], 1) == 0) {
         v.rhit[atomicAdd(&sh.n_rays, 1)] = r;
         atomicMin(&sh.k0, r);
@@ -413,7 +431,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     Views v;
     v.tlo = d.tile_lo; v.thi = d.tile_hi; v.tmaxd = d.tile_maxd; v.tstart = d.tile_start; v.thit = d.tiles_hit;
     v.ray_off = d.ray_off; v.ptS = d.ptS; v.prefix = d.prefix; v.cptS = d.cand_ptS; v.cprefix = d.cand_prefix;
-    v.tS = d.tS; v.sig = d.sig; v.rflag = d.ray_flag; v.rhit = d.rays_hit; v.ord = d.order;
+    v.tS = d.tS; v.sig = d.sig; v.rflag = d.ray_flag; v.rhit = d.rays_hit; v.ord = d.order; v.tray = d.tile_ray;
     v.chi = reinterpret_cast<double *>(lds + L.chi);
     if constexpr (SMALL) {
         float *a = reinterpret_cast<float *>(lds + L.tlo), *b = reinterpret_cast<float *>(lds + L.thi);
@@ -428,6 +446,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         }
         for (int i = tid; i < NT; i += kChainThreads) m[i] = d.tile_maxd[i];
         for (int i = tid; i <= NT; i += kChainThreads) ts[i] = d.tile_start[i];
+        int *tr = reinterpret_cast<int *>(lds + L.tray);
+        for (int i = tid; i < NT; i += kChainThreads) tr[i] = d.tile_ray[i];
+        v.tray = tr;
         for (int i = tid; i <= n; i += kChainThreads) ro[i] = d.ray_off[i];
         for (int i = tid; i < n; i += kChainThreads) {
             p[i] = d.ptS[i];
@@ -449,7 +470,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.iter = s0.iter;
         sh.evaluations = 0;
         sh.bytes = 0;
-        sh.grid_fallbacks = 0;
+        sh.grid_fallbacks32 = 0;
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
         sh.ncells = s0.ncells;
@@ -457,6 +478,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.nfree = s0.nfree;
         sh.clr_changed = sh.clr_rays = 0;
         sh.g_op = 0;
+        sh.grid_ovf = *d.grid_overflow;
         for (int k = 0; k < 16; ++k) sh.prof[k] = 0;
         sh.t_last = clock64();
     }
@@ -469,40 +491,36 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             if (wv == 0) draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
             __syncthreads();
         }
-        // ================= phase A: housekeeping + draw =================
+        if (prof_on && tid == 0) sh.t_iter = clock64();
+        // ===== phase A: last iteration's flags and grid update || the proposal =====
         for (int c = tid; c < sh.clr_changed; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
         for (int c = tid; c < sh.clr_rays; c += kChainThreads) v.rflag[v.rhit[c]] = 0;
         if (wv == kWaves - 1 && sh.g_op) {
             grid_apply(d, sh, lane);
             if (lane == 0) sh.g_op = 0;
         }
-        if (tid == 0) {
-            const int ncells = sh.ncells;
+        if (tid == 0) {  // TD_inversion_function.jl:72-80,127-128,184-188,221-232
+            const int nc = sh.ncells;
             const tdchain::Draws dr = draws[it & 63];
-            Proposal p = tdchain::propose(P, dr, ncells);
+            Proposal q = tdchain::propose(P, dr, nc);
             sh.slot_k = -1;
             sh.new_slot = -1;
-            if (p.active && p.action != tdchain::kBirth) {
-                const int s = v.ord[p.index];
+            if (q.active && q.action != tdchain::kBirth) {
+                const int s = v.ord[q.index];
                 const double x = d.cx[s], y = d.cy[s], z = d.cz[s], ze = d.czeta[s];
                 sh.slot_k = s;
                 sh.kx = x;
                 sh.ky = y;
                 sh.kz = z;
                 sh.zeta_killed = ze;
-                tdchain::complete_proposal(P, dr, p, x, y, z, ze);
+                tdchain::complete_proposal(P, dr, q, x, y, z, ze);
             }
-            if (p.active && p.action == tdchain::kBirth)
+            if (q.active && q.action == tdchain::kBirth)
                 sh.new_slot = sh.nfree > 0 ? d.free_slots[sh.nfree - 1] : sh.nslots;
-            if (p.active) sh.proposed[p.action] += 1;
-            if (p.active && (p.action == tdchain::kBirth || p.action == tdchain::kDeath)) {
-                sh.qx[0] = p.action == tdchain::kBirth ? p.x : sh.kx;
-                sh.qy[0] = p.action == tdchain::kBirth ? p.y : sh.ky;
-                sh.qz[0] = p.action == tdchain::kBirth ? p.z : sh.kz;
-            }
-            sh.p = p;
+            if (q.active) sh.proposed[q.action] += 1;
+            sh.p = q;
             // forward evaluation needed (birth validity is only known after its query)
-            sh.eval = p.active && (p.valid || p.action == tdchain::kBirth) && P.debug_prior != 1;
+            sh.eval = q.active && (q.valid || q.action == tdchain::kBirth) && P.debug_prior != 1;
             sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
             sh.pts_seen = sh.ray_pts = 0;
             sh.k0 = n;
@@ -512,237 +530,257 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         STAMP(0);
         const int action = sh.p.action;
         const int ncells = sh.ncells;
-        if (sh.p.active) {
-            Proposal p = sh.p;
-            const int slot_k = sh.slot_k;
-            const bool eval = sh.eval;
-            const double kx = sh.kx, ky = sh.ky, kz = sh.kz;
+        const Proposal p = sh.p;
+        const int slot_k = sh.slot_k;
+        const bool eval = sh.eval;
+        const double kx = sh.kx, ky = sh.ky, kz = sh.kz;
+        double czeta = 0.0, zetanew_death = 0.0;
+        if (p.active) {
             // ============ phase B: tile pass || birth/death Interpolation ============
+            const bool query = action == tdchain::kBirth || action == tdchain::kDeath;
             if (eval) {
+                // tiles whose box can hold a point the proposal changes (the last
+                // wave answers the Interpolation query meanwhile)
                 const bool q0 = action != tdchain::kBirth;  // old site of the selected cell
                 const bool q1 = action == tdchain::kBirth || action == tdchain::kMove;  // new site
-                for (int t = tid; t < NT; t += kChainThreads) {
-                    const double mx = v.tmaxd[t];
-                    bool hit = false;
-                    if (q0) hit = tile_lb2(v.tlo, v.thi, NT, t, kx, ky, kz) <= mx;
-                    if (q1 && !hit) hit = tile_lb2(v.tlo, v.thi, NT, t, p.x, p.y, p.z) <= mx;
-                    if (hit) v.thit[atomicAdd(&sh.n_tiles, 1)] = t;
-                }
+                const int nthr = query ? kChainThreads - 64 : kChainThreads;
+                if (tid < nthr)
+                    for (int t = tid; t < NT; t += nthr) {
+                        const double mx = v.tmaxd[t];
+                        bool hit = false;
+                        if (q0) hit = tile_lb2(v.tlo, v.thi, NT, t, kx, ky, kz) <= mx;
+                        if (q1 && !hit) hit = tile_lb2(v.tlo, v.thi, NT, t, p.x, p.y, p.z) <= mx;
+                        if (hit) v.thit[atomicAdd(&sh.n_tiles, 1)] = t;
+                    }
             }
             if (action == tdchain::kDeath)  // deleteat! shift, staged before we know if it is accepted
                 for (int j = (int)p.index + 1 + tid; j < ncells; j += kChainThreads) d.order_tmp[j] = v.ord[j];
-            double czeta = 0.0, zetanew_death = 0.0;
-            if (action == tdchain::kBirth || action == tdchain::kDeath) {
-                nearest_queries(d, v, sh, 1, action == tdchain::kDeath ? slot_k : -1, -1, 0.0, 0.0, 0.0);
-                if (action == tdchain::kBirth) {
-                    czeta = sh.res_z[0];                // TD_inversion_function.jl:81
-                    tdchain::birth_zeta(P, p, czeta);  // every lane, same value: no extra barrier
-                } else {
-                    zetanew_death = sh.res_z[0];  // :146
-                }
-            } else {
-                __syncthreads();  // tile list complete
+            if (query && wv == kWaves - 1) {  // TD_inversion_function.jl:81 (birth), :146 (death)
+                const bool birth = action == tdchain::kBirth;
+                const Nearest r = wave_nearest(d, v, sh, lane, birth ? p.x : kx, birth ? p.y : ky, birth ? p.z : kz,
+                                               birth ? -1 : slot_k, -1, 0.0, 0.0, 0.0);
+                if (lane == 0) sh.q_zeta = r.z;
             }
-            STAMP(1);
-            if (p.valid) {
-                double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
-                if (P.debug_prior != 1) {
-                    // ================= phase C: affected points =================
-                    const int nt = sh.n_tiles;
-                    const int rank_k = slot_k >= 0 ? d.rank[slot_k] : 0;
-                    const double zeta_k = slot_k >= 0 ? d.czeta[slot_k] : 0.0;
-                    int seen = 0;
-                    for (int item = tid; item < nt * kTilePts; item += kChainThreads) {
-                        const int t = v.thit[item / kTilePts];
-                        const int q = v.tstart[t] + item % kTilePts;
-                        if (q >= v.tstart[t + 1]) continue;
-                        ++seen;
-                        const int s = d.best_s[q];
-                        const double bd = d.best_d[q];
-                        if (action == tdchain::kBirth) {  // appended cell: strict capture
-                            const double dd = dist2(p.x, p.y, p.z, d.px[q], d.py[q], d.pz[q]);
-                            if (dd < bd) mark(d, v, sh, q, sh.new_slot, dd, p.zeta);
-                        } else if (action == tdchain::kChange) {
-                            if (s == slot_k) mark(d, v, sh, q, s, bd, p.zeta);
-                        } else if (s == slot_k) {  // death / move: its points are re-searched
-                            d.orphans[atomicAdd(&sh.n_orphans, 1)] = q;
-                        } else if (action == tdchain::kMove) {
-                            const double dd = dist2(p.x, p.y, p.z, d.px[q], d.py[q], d.pz[q]);
-                            if (dd < bd || (dd == bd && s >= 0 && rank_k < d.rank[s]))
-                                mark(d, v, sh, q, slot_k, dd, zeta_k);
-                        }
-                    }
-                    if (seen) atomicAdd(&sh.pts_seen, seen);
-                    __syncthreads();
-                    STAMP(2);
-                    // ========= phase D: re-search orphaned points, one wave each =========
-                    const int no = sh.n_orphans;
-                    const bool death = action == tdchain::kDeath;
-                    for (int o0 = 0; o0 < no; o0 += kBatch) {
-                        const int nq = min(kBatch, no - o0);
-                        if (tid < nq) {
-                            const int q = d.orphans[o0 + tid];
-                            sh.qx[tid] = d.px[q];
-                            sh.qy[tid] = d.py[q];
-                            sh.qz[tid] = d.pz[q];
-                        }
-                        __syncthreads();
-                        nearest_queries(d, v, sh, nq, death ? slot_k : -1, death ? -1 : slot_k, p.x, p.y, p.z);
-                        if (tid < nq)
-                            mark(d, v, sh, d.orphans[o0 + tid], sh.res_s[tid], sh.res_d[tid], sh.res_z[tid]);
-                        __syncthreads();
-                    }
-                    STAMP(3);
-                    // ================= phase E: t* of the rays that changed =================
-                    const int nr = sh.n_rays;
-                    const OverlayZeta oz{d.cand_flag, d.cand_z, d.zeta0};
-                    for (int rr = wv; rr < nr; rr += kWaves) {
-                        const int r = v.rhit[rr];
-                        const int s0 = v.ray_off[r];
-                        const int npr = v.ray_off[r + 1] - s0;
-                        const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
-                        if (lane == 0) {
-                            v.cptS[r] = val;
-                            atomicAdd(&sh.ray_pts, npr);
-                        }
-                    }
-                    __syncthreads();
-                    STAMP(4);
-                    // ========== phase F: chi^2 from the first changed ray on ==========
-                    // terms in parallel into LDS, then ONE lane adds them in k order
-                    // (MCsub.jl:170-172), 8 terms per LDS round trip
-                    const int k0 = sh.k0;
-                    double C = (tid == 0 && k0 > 0) ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
-                    for (int base = k0; base < n; base += chi_chunk) {
-                        const int cnt = min(chi_chunk, n - base);
-                        for (int k = tid; k < cnt; k += kChainThreads) {
-                            const int r = base + k;
-                            const double pt = v.rflag[r] ? v.cptS[r] : v.ptS[r];
-                            const double df = pt - v.tS[r];
-                            const double sg = v.sig[r];
-                            v.chi[k] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
-                        }
-                        __syncthreads();
-                        if (tid == 0) {
-                            int k = 0;
-                            for (; k + 8 <= cnt; k += 8) {
-                                double t[8], c[8];
-#pragma unroll
-                                for (int u = 0; u < 8; ++u) t[u] = v.chi[k + u];
-#pragma unroll
-                                for (int u = 0; u < 8; ++u) {
-                                    C = C + t[u];
-                                    c[u] = C;
-                                }
-#pragma unroll
-                                for (int u = 0; u < 8; ++u) v.cprefix[base + k + u] = c[u];
-                            }
-                            for (; k < cnt; ++k) {
-                                C = C + v.chi[k];
-                                v.cprefix[base + k] = C;
-                            }
-                        }
-                        if (base + chi_chunk < n) __syncthreads();  // the LDS terms are reused
-                    }
-                    phi_n = k0 < n ? C : sh.phi;
-                    if (tid == 0) {
-                        sh.evaluations += 1;
-                        // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
-                        // candidate points (coords + cached slot/distance, 36 B), grid queries
-                        // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
-                        // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
-                        sh.bytes += (long long)NT * 32 + (long long)sh.pts_seen * 36 +
-                                    (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
-                                    (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28;
+            __syncthreads();  // tile list complete, query answered
+            if (action == tdchain::kBirth) czeta = sh.q_zeta;
+            if (action == tdchain::kDeath) zetanew_death = sh.q_zeta;
+        }
+        Proposal pp = p;
+        if (p.active && action == tdchain::kBirth) tdchain::birth_zeta(P, pp, czeta);  // every lane, same value
+        STAMP(1);
+        if (pp.active && pp.valid) {
+            double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
+            if (P.debug_prior != 1) {
+                // ================= phase C: affected points =================
+                const int nt = sh.n_tiles;
+                const int rank_k = slot_k >= 0 ? d.rank[slot_k] : 0;
+                const double zeta_k = slot_k >= 0 ? d.czeta[slot_k] : 0.0;
+                int seen = 0;
+                for (int item = tid; item < nt * kTilePts; item += kChainThreads) {
+                    const int t = v.thit[item / kTilePts];
+                    const int q = v.tstart[t] + item % kTilePts;
+                    if (q >= v.tstart[t + 1]) continue;
+                    ++seen;
+                    const int ray = v.tray[t];
+                    // independent loads: one round trip
+                    const int s = d.best_s[q];
+                    const double bd = d.best_d[q];
+                    const double qx = d.px[q], qy = d.py[q], qz = d.pz[q];
+                    if (action == tdchain::kBirth) {  // appended cell: strict capture
+                        const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
+                        if (dd < bd) mark(d, v, sh, q, ray, sh.new_slot, dd, pp.zeta);
+                    } else if (action == tdchain::kChange) {
+                        if (s == slot_k) mark(d, v, sh, q, ray, s, bd, pp.zeta);
+                    } else if (s == slot_k) {  // death / move: its points are re-searched
+                        const int o = atomicAdd(&sh.n_orphans, 1);
+                        d.orphans[o] = q;
+                        if (o < kOrphanLds) sh.orph[o] = OrphanRec{qx, qy, qz, q, ray};
+                    } else if (action == tdchain::kMove) {
+                        const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
+                        if (dd < bd || (dd == bd && s >= 0 && rank_k < d.rank[s]))
+                            mark(d, v, sh, q, ray, slot_k, dd, zeta_k);
                     }
                 }
-                // ================= Metropolis-Hastings decision =================
-                if (tid == 0) {
-                    const bool acc = tdchain::accept(P, p, ncells, sh.phi, phi_n, czeta, sh.zeta_killed,
-                                                     zetanew_death);
-                    sh.accept = acc ? 1 : 0;
-                    sh.phi_n = phi_n;
-                    if (acc) sh.accepted[action] += 1;
+                if (seen) atomicAdd(&sh.pts_seen, seen);
+                __syncthreads();
+                STAMP(2);
+                // ========= phase D: re-search orphaned points, one wave each =========
+                const int no = sh.n_orphans;
+                const bool death = action == tdchain::kDeath;
+                for (int o = wv; o < no; o += kWaves) {  // one wave per orphan, no block barrier
+                    double qx, qy, qz;
+                    int q, ray;
+                    if (o < kOrphanLds) {
+                        qx = sh.orph[o].x;
+                        qy = sh.orph[o].y;
+                        qz = sh.orph[o].z;
+                        q = sh.orph[o].q;
+                        ray = sh.orph[o].ray;
+                    } else {
+                        q = d.orphans[o];
+                        qx = d.px[q];
+                        qy = d.py[q];
+                        qz = d.pz[q];
+                        ray = d.pt_ray[q];
+                    }
+                    const Nearest r = wave_nearest(d, v, sh, lane, qx, qy, qz, death ? slot_k : -1,
+                                                   death ? -1 : slot_k, pp.x, pp.y, pp.z);
+                    if (lane == 0) mark(d, v, sh, q, ray, r.s, r.d, r.z);
+                }
+                if (no > 0) __syncthreads();
+                STAMP(3);
+                // ================= phase E: t* of the rays that changed =================
+                const int nr = sh.n_rays;
+                const OverlayZeta oz{d.cand_flag, d.cand_z, d.zeta0};
+                for (int rr = wv; rr < nr; rr += kWaves) {
+                    const int r = v.rhit[rr];
+                    const int s0 = v.ray_off[r];
+                    const int npr = v.ray_off[r + 1] - s0;
+                    const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
+                    if (lane == 0) {
+                        v.cptS[r] = val;
+                        atomicAdd(&sh.ray_pts, npr);
+                    }
                 }
                 __syncthreads();
-                STAMP(5);
-                // ================= phase G: commit =================
-                if (sh.accept) {
-                    const int nc = sh.n_changed, nr = sh.n_rays, nt = sh.n_tiles, k0 = sh.k0;
-                    for (int c = tid; c < nc; c += kChainThreads) {
-                        const int q = d.changed[c];
-                        d.best_s[q] = d.cand_s[q];
-                        d.best_d[q] = d.cand_d[q];
-                        d.zeta0[q] = d.cand_z[q];
+                STAMP(4);
+                // ========== phase F: chi^2 from the first changed ray on ==========
+                // terms in parallel into LDS, then ONE lane adds them in k order
+                // (MCsub.jl:170-172), 8 terms per LDS round trip
+                const int k0 = sh.k0;
+                double C = (tid == 0 && k0 > 0) ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
+                for (int base = k0; base < n; base += chi_chunk) {
+                    const int cnt = min(chi_chunk, n - base);
+                    for (int k = tid; k < cnt; k += kChainThreads) {
+                        const int r = base + k;
+                        const double pt = v.rflag[r] ? v.cptS[r] : v.ptS[r];
+                        const double df = pt - v.tS[r];
+                        const double sg = v.sig[r];
+                        v.chi[k] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                     }
-                    // tile maxima of the new distances (changed points lie in hit tiles;
-                    // the overlay reads the new value whether or not it is committed yet)
-                    if (P.debug_prior != 1 && action != tdchain::kChange)
-                        for (int i = tid; i < nt * kTilePts; i += kChainThreads) {  // 16 lanes per tile
-                            const int t = v.thit[i / kTilePts];
-                            const int q = v.tstart[t] + (i % kTilePts);
-                            double mx = -1.0;
-                            if (q < v.tstart[t + 1]) mx = d.cand_flag[q] ? d.cand_d[q] : d.best_d[q];
-#pragma unroll
-                            for (int off = kTilePts / 2; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
-                            if ((i % kTilePts) == 0) v.tmaxd[t] = mx;
-                        }
-                    for (int rr = tid; rr < nr; rr += kChainThreads) {
-                        const int r = v.rhit[rr];
-                        v.ptS[r] = v.cptS[r];
-                    }
-                    for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
-                    if (action == tdchain::kDeath)  // deleteat!: positions after the killed one shift down
-                        for (int j = (int)p.index + 1 + tid; j < ncells; j += kChainThreads) {
-                            const int s = d.order_tmp[j];
-                            v.ord[j - 1] = s;
-                            d.rank[s] = j - 1;
-                        }
+                    __syncthreads();
                     if (tid == 0) {
-                        const int sk = sh.slot_k;
-                        if (action == tdchain::kBirth) {  // append!
-                            const int s = sh.new_slot;
-                            d.cx[s] = p.x;
-                            d.cy[s] = p.y;
-                            d.cz[s] = p.z;
-                            d.czeta[s] = p.zeta;
-                            v.ord[ncells] = s;
-                            d.rank[s] = ncells;
-                            if (sh.nfree > 0)
-                                sh.nfree -= 1;
-                            else
-                                sh.nslots += 1;
-                            sh.ncells = ncells + 1;
-                            sh.g_op = 2;
-                            sh.g_slot = s;
-                        } else if (action == tdchain::kDeath) {
-                            d.free_slots[sh.nfree] = sk;
-                            sh.nfree += 1;
-                            d.rank[sk] = -1;
-                            sh.ncells = ncells - 1;
-                            sh.g_op = 1;
-                            sh.g_slot = sk;
-                        } else if (action == tdchain::kChange) {
-                            d.czeta[sk] = p.zeta;
-                        } else {
-                            d.cx[sk] = p.x;
-                            d.cy[sk] = p.y;
-                            d.cz[sk] = p.z;
-                            sh.g_op = 3;
-                            sh.g_slot = sk;
+                        int k = 0;
+                        for (; k + 8 <= cnt; k += 8) {
+                            double t[8], c[8];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) t[u] = v.chi[k + u];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                C = C + t[u];
+                                c[u] = C;
+                            }
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) v.cprefix[base + k + u] = c[u];
                         }
-                        sh.g_ox = sh.kx;
-                        sh.g_oy = sh.ky;
-                        sh.g_oz = sh.kz;
-                        sh.g_nx = p.x;
-                        sh.g_ny = p.y;
-                        sh.g_nz = p.z;
-                        sh.phi = sh.phi_n;
+                        for (; k < cnt; ++k) {
+                            C = C + v.chi[k];
+                            v.cprefix[base + k] = C;
+                        }
                     }
+                    if (base + chi_chunk < n) __syncthreads();  // the LDS terms are reused
+                }
+                phi_n = k0 < n ? C : sh.phi;
+                if (tid == 0) {
+                    sh.evaluations += 1;
+                    // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
+                    // candidate points (coords + cached slot/distance, 36 B), grid queries
+                    // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
+                    // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
+                    sh.bytes += (long long)NT * 32 + (long long)sh.pts_seen * 36 +
+                                (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
+                                (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28;
+                }
+            }
+            // ================= Metropolis-Hastings decision =================
+            if (tid == 0) {
+                const bool acc = tdchain::accept(P, pp, ncells, sh.phi, phi_n, czeta, sh.zeta_killed,
+                                                 zetanew_death);
+                sh.accept = acc ? 1 : 0;
+                sh.phi_n = phi_n;
+                if (acc) sh.accepted[action] += 1;
+            }
+            __syncthreads();
+            STAMP(5);
+            // ================= phase G: commit =================
+            if (sh.accept) {
+                const int nc = sh.n_changed, nr = sh.n_rays, nt = sh.n_tiles, k0 = sh.k0;
+                for (int c = tid; c < nc; c += kChainThreads) {
+                    const int q = d.changed[c];
+                    d.best_s[q] = d.cand_s[q];
+                    d.best_d[q] = d.cand_d[q];
+                    d.zeta0[q] = d.cand_z[q];
+                }
+                // tile maxima of the new distances (changed points lie in hit tiles;
+                // the overlay reads the new value whether or not it is committed yet)
+                if (P.debug_prior != 1 && action != tdchain::kChange)
+                    for (int i = tid; i < nt * kTilePts; i += kChainThreads) {  // 16 lanes (a DPP row) per tile
+                        const int t = v.thit[i / kTilePts];
+                        const int q = v.tstart[t] + (i % kTilePts);
+                        unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
+                        if (q < v.tstart[t + 1]) {
+                            const double cd = d.cand_d[q], bd = d.best_d[q];
+                            mk = (unsigned long long)__double_as_longlong(d.cand_flag[q] ? cd : bd);
+                        }
+                        mk = row_max_u64(mk);  // a tile = one DPP row of 16 lanes
+                        if ((i % kTilePts) == kTilePts - 1) v.tmaxd[t] = __longlong_as_double((long long)mk);
+                    }
+                for (int rr = tid; rr < nr; rr += kChainThreads) {
+                    const int r = v.rhit[rr];
+                    v.ptS[r] = v.cptS[r];
+                }
+                for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
+                if (action == tdchain::kDeath)  // deleteat!: positions after the killed one shift down
+                    for (int j = (int)pp.index + 1 + tid; j < ncells; j += kChainThreads) {
+                        const int s = d.order_tmp[j];
+                        v.ord[j - 1] = s;
+                        d.rank[s] = j - 1;
+                    }
+                if (tid == 0) {
+                    const int sk = sh.slot_k;
+                    if (action == tdchain::kBirth) {  // append!
+                        const int s = sh.new_slot;
+                        d.cx[s] = pp.x;
+                        d.cy[s] = pp.y;
+                        d.cz[s] = pp.z;
+                        d.czeta[s] = pp.zeta;
+                        v.ord[ncells] = s;
+                        d.rank[s] = ncells;
+                        if (sh.nfree > 0)
+                            sh.nfree -= 1;
+                        else
+                            sh.nslots += 1;
+                        sh.ncells = ncells + 1;
+                        sh.g_op = 2;
+                        sh.g_slot = s;
+                    } else if (action == tdchain::kDeath) {
+                        d.free_slots[sh.nfree] = sk;
+                        sh.nfree += 1;
+                        d.rank[sk] = -1;
+                        sh.ncells = ncells - 1;
+                        sh.g_op = 1;
+                        sh.g_slot = sk;
+                    } else if (action == tdchain::kChange) {
+                        d.czeta[sk] = pp.zeta;
+                    } else {
+                        d.cx[sk] = pp.x;
+                        d.cy[sk] = pp.y;
+                        d.cz[sk] = pp.z;
+                        sh.g_op = 3;
+                        sh.g_slot = sk;
+                    }
+                    sh.g_ox = sh.kx;
+                    sh.g_oy = sh.ky;
+                    sh.g_oz = sh.kz;
+                    sh.g_nx = pp.x;
+                    sh.g_ny = pp.y;
+                    sh.g_nz = pp.z;
+                    sh.phi = sh.phi_n;
                 }
             }
         }
         if (tid == 0) {
+            if (prof_on) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
             sh.iter += 1;
             sh.clr_changed = sh.n_changed;
             sh.clr_rays = sh.n_rays;
@@ -777,7 +815,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         s.nslots = sh.nslots;
         s.nfree = sh.nfree;
         for (int k = 0; k < 15; ++k) s.prof[k] += sh.prof[k];
-        s.prof[15] += sh.grid_fallbacks;  // diagnostic: unproven grid searches
+        s.prof[15] += sh.grid_fallbacks32;  // diagnostic: unproven grid searches
     }
 }
 

@@ -17,8 +17,8 @@ sys.path.insert(0, ROOT)
 import tonga  # noqa: E402
 
 # k_chain_run phases A..G (chain_kernels.hip, STAMP(0..6))
-PHASES = ["A draw", "B tiles + birth/death query", "C points", "D orphans", "E ray sums", "F chi2 + accept",
-          "G commit"]
+PHASES = ["A draw + flags + grid update", "B tiles + birth/death query", "C points", "D orphans", "E ray sums",
+          "F chi2 + accept", "G commit"]
 
 
 def main():
@@ -33,6 +33,7 @@ def main():
     L = tt.lib()
     out0 = (ctypes.c_int64 * 16)()
     L.tdt_chain_profile(ch.h, 1, out0)
+    st0 = ch.stats()
     t0 = time.perf_counter()
     ch.run(iters)
     el = time.perf_counter() - t0
@@ -41,10 +42,15 @@ def main():
     cyc = np.array(out[:7], dtype=np.float64) - np.array(out0[:7], dtype=np.float64)
     fallbacks = int(out[15] - out0[15])
     tot = cyc.sum()
+    st1 = ch.stats()
+    prop = np.array(st1["proposed"], dtype=np.float64) - np.array(st0["proposed"], dtype=np.float64)
+    act = np.array(out[8:12], dtype=np.float64) - np.array(out0[8:12], dtype=np.float64)
+    per_action = {a: round(c / max(k, 1), 1) for a, c, k in zip(["birth", "death", "change", "move"], act, prop)}
     res = {"cells": N, "iters": iters, "us_per_iter_wall": el / iters * 1e6,
            "cycles_per_iter": tot / iters, "grid_fallbacks": fallbacks,
            "phases": {p: {"share": round(c / tot, 4), "cycles_per_iter": round(c / iters, 1)}
-                      for p, c in zip(PHASES, cyc)}}
+                      for p, c in zip(PHASES, cyc)},
+           "cycles_per_proposal_by_action": per_action}
     print(json.dumps(res, indent=1))
 
 
