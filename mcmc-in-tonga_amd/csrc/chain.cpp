@@ -229,12 +229,12 @@ int device_setup(td_chain *ch) {
     auto add = [&](size_t b) { bytes += ((b + 255) / 256) * 256; };
     const size_t Pn = (size_t)std::max<int64_t>(P, 1), nn = (size_t)std::max<int64_t>(n, 1);
     add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * Pn);
-    add(sizeof(float) * 3 * ntiles); add(sizeof(float) * 3 * ntiles); add(sizeof(double) * (ntiles + 1));
+    add(sizeof(float) * 3 * ntiles); add(sizeof(float) * 3 * ntiles); add(sizeof(double) * (ntiles + 1)); add(sizeof(double) * (ntiles + 1));
     add(sizeof(double) * 4 * cap); for (int i = 0; i < 4; ++i) add(sizeof(int) * cap);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn); add(Pn);
     add(sizeof(int) * Pn); add(sizeof(int) * Pn); add(sizeof(int) * (ntiles + 1));
-    for (int i = 0; i < 4; ++i) add(sizeof(double) * nn);
+    for (int i = 0; i < 6; ++i) add(sizeof(double) * nn);
     add(sizeof(int) * nn); add(sizeof(int) * nn); add(sizeof(ChainScalars));
     add(sizeof(int) * nbuckets); add(sizeof(BucketEntry) * nbuckets * kBucketCap); add(sizeof(int));
     add(sizeof(DevChain));
@@ -255,6 +255,7 @@ int device_setup(td_chain *ch) {
     float *thi = carve<float>(cur, 3 * (size_t)ntiles);
     d.tile_start = tile_start; d.tile_ray = tile_ray_d; d.pt_ray = pt_ray_d; d.tile_lo = tlo; d.tile_hi = thi;
     d.tile_maxd = carve<double>(cur, ntiles + 1);
+    d.tile_cmax = carve<double>(cur, ntiles + 1);
     d.ntiles = ntiles;
     double *cells = carve<double>(cur, 4 * (size_t)cap);
     d.cx = cells; d.cy = cells + cap; d.cz = cells + 2 * cap; d.czeta = cells + 3 * cap;
@@ -267,6 +268,7 @@ int device_setup(td_chain *ch) {
     d.changed = carve<int>(cur, Pn); d.orphans = carve<int>(cur, Pn); d.tiles_hit = carve<int>(cur, ntiles + 1);
     d.ptS = carve<double>(cur, nn); d.cand_ptS = carve<double>(cur, nn);
     d.prefix = carve<double>(cur, nn); d.cand_prefix = carve<double>(cur, nn);
+    d.term = carve<double>(cur, nn); d.cand_term = carve<double>(cur, nn);
     d.rays_hit = carve<int>(cur, nn); d.ray_flag = carve<int>(cur, nn);
     d.st = carve<ChainScalars>(cur, 1);
     d.grid = G;

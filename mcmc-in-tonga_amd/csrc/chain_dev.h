@@ -78,6 +78,7 @@ struct DevChain {
     const int *tile_ray;              // [ntiles] ray of each tile
     const float *tile_lo, *tile_hi;   // [3][ntiles] SoA, outward-rounded to FP32
     double *tile_maxd;                // [ntiles] max cached distance of the tile's points
+    double *tile_cmax;                // [ntiles] scratch: hit tiles' maxima if accepted
     int ntiles;
     // cells by slot
     double *cx, *cy, *cz, *czeta;  // [cap]
@@ -92,6 +93,7 @@ struct DevChain {
     int *changed, *orphans, *tiles_hit;
     // rays
     double *ptS, *cand_ptS, *prefix, *cand_prefix;  // prefix[k] = chi^2 partial sum through ray k
+    double *term, *cand_term;                       // chi^2 term of each ray (MCsub.jl:171)
     int *rays_hit;
     int *ray_flag;
     ChainScalars *st;

@@ -116,14 +116,48 @@ struct OverlayZeta {
     }
 };
 
-struct Shared {
+// A proposal with what it needs from the model (tid 0 builds it).
+struct PState {
     Proposal p;
-    double czeta, zeta_killed, zetanew_death, kx, ky, kz, phi_n;
-    int slot_k, new_slot, accept, eval;
+    double kx, ky, kz, zeta_killed;  // site and value of the selected cell (not birth)
+    int slot_k, new_slot, eval;
+};
+
+// TD_inversion_function.jl:72-80,127-128,184-188,221-232: the proposal of one
+// iteration from its draws and the model.  slot_at(pos) = slot at Julia
+// position pos.
+template <class SlotAt>
+__device__ __forceinline__ void make_proposal(PState &o, const tdchain::Params &P, const tdchain::Draws &dr,
+                                              int ncells, int nfree, int nslots, const int *free_slots,
+                                              const double *cx, const double *cy, const double *cz,
+                                              const double *czeta, SlotAt slot_at) {
+    Proposal q = tdchain::propose(P, dr, ncells);
+    o.slot_k = -1;
+    o.new_slot = -1;
+    if (q.active && q.action != tdchain::kBirth) {
+        const int s = slot_at((int)q.index);
+        const double x = cx[s], y = cy[s], z = cz[s], ze = czeta[s];
+        o.slot_k = s;
+        o.kx = x;
+        o.ky = y;
+        o.kz = z;
+        o.zeta_killed = ze;
+        tdchain::complete_proposal(P, dr, q, x, y, z, ze);
+    }
+    if (q.active && q.action == tdchain::kBirth) o.new_slot = nfree > 0 ? free_slots[nfree - 1] : nslots;
+    o.p = q;
+    // forward evaluation needed (birth validity is only known after its query)
+    o.eval = q.active && (q.valid || q.action == tdchain::kBirth) && P.debug_prior != 1;
+}
+
+struct Shared {
+    PState cur, spec;  // this iteration's proposal; the next one, guessed during phase F
+    int spec_ok;
+    double phi_n;
+    int accept;
     int n_tiles, n_changed, n_orphans, n_rays, k0;
-    int clr_changed, clr_rays;  // flags to clear at the start of the next iteration
     int pts_seen, ray_pts;
-    // pending bucket-grid update (applied by the last wave next iteration)
+    // bucket-grid update of an accepted proposal (applied by the last wave in phase G)
     int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site
     double g_ox, g_oy, g_oz, g_nx, g_ny, g_nz;
     // chain scalars, resident for the whole launch
@@ -151,8 +185,8 @@ struct Shared {
 
 // LDS carve-up (host and device agree on it through this function).
 struct LdsPlan {
-    size_t scratch, chi, draws, tlo, thi, tmaxd, tstart, thit, tray, rayoff, ptS, prefix, cptS, cprefix, tS, sig,
-        rflag, rhit, ord, total;
+    size_t scratch, draws, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
+        tS, sig, rflag, rhit, ord, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -161,7 +195,6 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
     LdsPlan L{};
     size_t o = align16(sizeof(Shared));
     L.scratch = o; o += align16(sizeof(double) * kWaves * 96);
-    L.chi = o; o += align16(sizeof(double) * (small ? (n > 0 ? n : 1) : 2048));  // chi^2 terms
     L.draws = o; o += align16(sizeof(tdchain::Draws) * 64);                     // 64 iterations ahead
     if (small) {
         L.tlo = o; o += align16(sizeof(float) * 3 * ntiles);
@@ -169,12 +202,15 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
         L.tmaxd = o; o += align16(sizeof(double) * ntiles);
         L.tstart = o; o += align16(sizeof(int) * (ntiles + 1));
         L.thit = o; o += align16(sizeof(int) * (ntiles + 1));
+        L.ctm = o; o += align16(sizeof(double) * (ntiles + 1));
         L.tray = o; o += align16(sizeof(int) * ntiles);
         L.rayoff = o; o += align16(sizeof(int) * (n + 1));
         L.ptS = o; o += align16(sizeof(double) * n);
         L.prefix = o; o += align16(sizeof(double) * n);
         L.cptS = o; o += align16(sizeof(double) * n);
         L.cprefix = o; o += align16(sizeof(double) * n);
+        L.term = o; o += align16(sizeof(double) * n);
+        L.cterm = o; o += align16(sizeof(double) * n);
         L.tS = o; o += align16(sizeof(double) * n);
         L.sig = o; o += align16(sizeof(double) * n);
         L.rflag = o; o += align16(sizeof(int) * n);
@@ -188,7 +224,7 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
 // Views of the arrays a launch works on: LDS copies in SMALL mode, else HBM.
 struct Views {
     const float *tlo, *thi;
-    double *tmaxd, *ptS, *prefix, *cptS, *cprefix, *chi;
+    double *tmaxd, *ctm, *ptS, *prefix, *cptS, *cprefix, *term, *cterm;
     const double *tS, *sig;
     const int *tstart, *ray_off, *tray;
     int *thit, *rflag, *rhit, *ord;
@@ -398,20 +434,40 @@ __device__ __forceinline__ void mark(const DevChain &d, const Views &v, Shared &
     }
 }
 
-// Lower bound of dist2(q, p) over every point p of a tile.  The box is rounded
-// outward to FP32 and the gaps are computed in FP64 with the same rounded
-// operations as the distance, so lb2 <= dist2 holds bit-wise.
-__device__ __forceinline__ double tile_lb2(const float *lo, const float *hi, int nt, int t, double qx, double qy,
-                                           double qz) {
-    auto gap = [](double q, double l, double h) { return q < l ? l - q : (q > h ? q - h : 0.0); };
-    const double gx = gap(qx, (double)lo[t], (double)hi[t]);
-    const double gy = gap(qy, (double)lo[nt + t], (double)hi[nt + t]);
-    const double gz = gap(qz, (double)lo[2 * nt + t], (double)hi[2 * nt + t]);
-    double s = gx * gx;
+// Tile test in FP32: can some point p of tile t have dist2(q, p) <= thr?
+// Every rounding is taken against the answer (the query rounded to FP32 moves
+// by <= |q| 2^-24, each FP32 operation errs by <= 2^-24 relative), so the test
+// never says "no" for a tile that holds such a point; it may say "yes" for a
+// tile that does not (its points are then checked exactly in FP64).
+struct TileQuery {
+    float x, y, z, ex, ey, ez;  // coordinates and their rounding allowance
+};
+__device__ __forceinline__ TileQuery tile_query(double x, double y, double z) {
+    TileQuery q;
+    q.x = (float)x;
+    q.y = (float)y;
+    q.z = (float)z;
+    q.ex = fabsf(q.x) * 0x1p-23f;
+    q.ey = fabsf(q.y) * 0x1p-23f;
+    q.ez = fabsf(q.z) * 0x1p-23f;
+    return q;
+}
+__device__ __forceinline__ float gap_lb(float q, float e, float l, float h) {
+    const float g = fmaxf(fmaxf(l - q, q - h), 0.0f);
+    return fmaxf(g * (1.0f - 0x1p-20f) - e, 0.0f);
+}
+// thr: an FP32 bound >= the FP64 threshold (tile_thr)
+__device__ __forceinline__ bool tile_may_hit(const float *lo, const float *hi, int nt, int t, const TileQuery &q,
+                                             float thr) {
+    const float gx = gap_lb(q.x, q.ex, lo[t], hi[t]);
+    const float gy = gap_lb(q.y, q.ey, lo[nt + t], hi[nt + t]);
+    const float gz = gap_lb(q.z, q.ez, lo[2 * nt + t], hi[2 * nt + t]);
+    float s = gx * gx;
     s = s + gy * gy;
     s = s + gz * gz;
-    return s;
+    return s * (1.0f - 0x1p-20f) <= thr;
 }
+__device__ __forceinline__ float tile_thr(double mx) { return (float)mx * (1.0f + 0x1p-20f); }
 
 template <bool SMALL>
 __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters) {
@@ -425,14 +481,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const tdchain::Params &P = d.params;
     const int n = d.n, NT = d.ntiles;
     const bool prof_on = d.profile != 0;
-    const int chi_chunk = SMALL ? n : 2048;
 
     // ---- views: LDS copies of the tile / ray / order arrays when they fit ----
     Views v;
     v.tlo = d.tile_lo; v.thi = d.tile_hi; v.tmaxd = d.tile_maxd; v.tstart = d.tile_start; v.thit = d.tiles_hit;
     v.ray_off = d.ray_off; v.ptS = d.ptS; v.prefix = d.prefix; v.cptS = d.cand_ptS; v.cprefix = d.cand_prefix;
     v.tS = d.tS; v.sig = d.sig; v.rflag = d.ray_flag; v.rhit = d.rays_hit; v.ord = d.order; v.tray = d.tile_ray;
-    v.chi = reinterpret_cast<double *>(lds + L.chi);
+    v.term = d.term;
+    v.cterm = d.cand_term;
+    v.ctm = d.tile_cmax;
     if constexpr (SMALL) {
         float *a = reinterpret_cast<float *>(lds + L.tlo), *b = reinterpret_cast<float *>(lds + L.thi);
         double *m = reinterpret_cast<double *>(lds + L.tmaxd);
@@ -462,8 +519,19 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         v.sig = sg; v.rflag = rf; v.ord = od;
         v.cptS = reinterpret_cast<double *>(lds + L.cptS);
         v.cprefix = reinterpret_cast<double *>(lds + L.cprefix);
+        v.term = reinterpret_cast<double *>(lds + L.term);
+        v.cterm = reinterpret_cast<double *>(lds + L.cterm);
         v.thit = reinterpret_cast<int *>(lds + L.thit);
+        v.ctm = reinterpret_cast<double *>(lds + L.ctm);
         v.rhit = reinterpret_cast<int *>(lds + L.rhit);
+        __syncthreads();  // ptS, tS, sig mirrored
+    }
+    // chi^2 term of every ray in the current state (MCsub.jl:171), cached: a
+    // proposal recomputes only the terms of the rays it changes
+    for (int r = tid; r < n; r += kChainThreads) {
+        const double df = v.ptS[r] - v.tS[r];
+        const double sg = v.sig[r];
+        v.term[r] = ((df * df) * 1.0) / (sg * sg);
     }
     if (tid == 0) {
         const ChainScalars &s0 = *d.st;
@@ -476,7 +544,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.ncells = s0.ncells;
         sh.nslots = s0.nslots;
         sh.nfree = s0.nfree;
-        sh.clr_changed = sh.clr_rays = 0;
         sh.g_op = 0;
         sh.grid_ovf = *d.grid_overflow;
         for (int k = 0; k < 16; ++k) sh.prof[k] = 0;
@@ -484,57 +551,34 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     }
     __syncthreads();
 
-    for (long long it = 0; it < iters; ++it) {
-        // ---- the RNG draws (and their normal quantiles) of the next 64
-        //      iterations, one lane each: a function of (seed, chain, iteration) ----
-        if ((it & 63) == 0) {
-            if (wv == 0) draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
-            __syncthreads();
-        }
-        if (prof_on && tid == 0) sh.t_iter = clock64();
-        // ===== phase A: last iteration's flags and grid update || the proposal =====
-        for (int c = tid; c < sh.clr_changed; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
-        for (int c = tid; c < sh.clr_rays; c += kChainThreads) v.rflag[v.rhit[c]] = 0;
-        if (wv == kWaves - 1 && sh.g_op) {
-            grid_apply(d, sh, lane);
-            if (lane == 0) sh.g_op = 0;
-        }
-        if (tid == 0) {  // TD_inversion_function.jl:72-80,127-128,184-188,221-232
-            const int nc = sh.ncells;
-            const tdchain::Draws dr = draws[it & 63];
-            Proposal q = tdchain::propose(P, dr, nc);
-            sh.slot_k = -1;
-            sh.new_slot = -1;
-            if (q.active && q.action != tdchain::kBirth) {
-                const int s = v.ord[q.index];
-                const double x = d.cx[s], y = d.cy[s], z = d.cz[s], ze = d.czeta[s];
-                sh.slot_k = s;
-                sh.kx = x;
-                sh.ky = y;
-                sh.kz = z;
-                sh.zeta_killed = ze;
-                tdchain::complete_proposal(P, dr, q, x, y, z, ze);
-            }
-            if (q.active && q.action == tdchain::kBirth)
-                sh.new_slot = sh.nfree > 0 ? d.free_slots[sh.nfree - 1] : sh.nslots;
-            if (q.active) sh.proposed[q.action] += 1;
-            sh.p = q;
-            // forward evaluation needed (birth validity is only known after its query)
-            sh.eval = q.active && (q.valid || q.action == tdchain::kBirth) && P.debug_prior != 1;
+    // the draws (and their normal quantiles) of 64 iterations, one lane each:
+    // a function of (seed, chain, iteration) only; and the first proposal
+    if (wv == 0) {
+        draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
+        wave_sync_lds();
+        if (lane == 0 && iters > 0) {
+            make_proposal(sh.cur, P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
+                          d.czeta, [&](int pos) { return v.ord[pos]; });
+            if (sh.cur.p.active) sh.proposed[sh.cur.p.action] += 1;
             sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
             sh.pts_seen = sh.ray_pts = 0;
             sh.k0 = n;
             sh.accept = 0;
         }
-        __syncthreads();
-        STAMP(0);
-        const int action = sh.p.action;
+        if (lane == 0) sh.spec_ok = 0;
+    }
+    __syncthreads();
+
+    for (long long it = 0; it < iters; ++it) {
+        if (prof_on && tid == 0) sh.t_iter = clock64();
+        const Proposal p = sh.cur.p;
+        const int action = p.action;
         const int ncells = sh.ncells;
-        const Proposal p = sh.p;
-        const int slot_k = sh.slot_k;
-        const bool eval = sh.eval;
-        const double kx = sh.kx, ky = sh.ky, kz = sh.kz;
+        const int slot_k = sh.cur.slot_k;
+        const bool eval = sh.cur.eval != 0;
+        const double kx = sh.cur.kx, ky = sh.cur.ky, kz = sh.cur.kz;
         double czeta = 0.0, zetanew_death = 0.0;
+        STAMP(0);
         if (p.active) {
             // ============ phase B: tile pass || birth/death Interpolation ============
             const bool query = action == tdchain::kBirth || action == tdchain::kDeath;
@@ -543,13 +587,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // wave answers the Interpolation query meanwhile)
                 const bool q0 = action != tdchain::kBirth;  // old site of the selected cell
                 const bool q1 = action == tdchain::kBirth || action == tdchain::kMove;  // new site
+                const TileQuery tq0 = tile_query(kx, ky, kz), tq1 = tile_query(p.x, p.y, p.z);
                 const int nthr = query ? kChainThreads - 64 : kChainThreads;
                 if (tid < nthr)
                     for (int t = tid; t < NT; t += nthr) {
-                        const double mx = v.tmaxd[t];
-                        bool hit = false;
-                        if (q0) hit = tile_lb2(v.tlo, v.thi, NT, t, kx, ky, kz) <= mx;
-                        if (q1 && !hit) hit = tile_lb2(v.tlo, v.thi, NT, t, p.x, p.y, p.z) <= mx;
+                        const float thr = tile_thr(v.tmaxd[t]);
+                        const bool hit = (q0 && tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr)) ||
+                                         (q1 && tile_may_hit(v.tlo, v.thi, NT, t, tq1, thr));
                         if (hit) v.thit[atomicAdd(&sh.n_tiles, 1)] = t;
                     }
             }
@@ -568,9 +612,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         Proposal pp = p;
         if (p.active && action == tdchain::kBirth) tdchain::birth_zeta(P, pp, czeta);  // every lane, same value
         STAMP(1);
+        // the next iteration's proposal can be guessed during phase F if its draws are here
+        const bool can_spec = it + 1 < iters && ((it + 1) & 63) != 0;
         if (pp.active && pp.valid) {
-            double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
-            if (P.debug_prior != 1) {
+            const bool fwd = P.debug_prior != 1;
+            int no = 0;
+            if (fwd) {
                 // ================= phase C: affected points =================
                 const int nt = sh.n_tiles;
                 const int rank_k = slot_k >= 0 ? d.rank[slot_k] : 0;
@@ -588,7 +635,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     const double qx = d.px[q], qy = d.py[q], qz = d.pz[q];
                     if (action == tdchain::kBirth) {  // appended cell: strict capture
                         const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
-                        if (dd < bd) mark(d, v, sh, q, ray, sh.new_slot, dd, pp.zeta);
+                        if (dd < bd) mark(d, v, sh, q, ray, sh.cur.new_slot, dd, pp.zeta);
                     } else if (action == tdchain::kChange) {
                         if (s == slot_k) mark(d, v, sh, q, ray, s, bd, pp.zeta);
                     } else if (s == slot_k) {  // death / move: its points are re-searched
@@ -605,7 +652,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 __syncthreads();
                 STAMP(2);
                 // ========= phase D: re-search orphaned points, one wave each =========
-                const int no = sh.n_orphans;
+                no = sh.n_orphans;
                 const bool death = action == tdchain::kDeath;
                 for (int o = wv; o < no; o += kWaves) {  // one wave per orphan, no block barrier
                     double qx, qy, qz;
@@ -639,49 +686,42 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
                     if (lane == 0) {
                         v.cptS[r] = val;
+                        const double df = val - v.tS[r];
+                        const double sg = v.sig[r];
+                        v.cterm[r] = v.term[r];                      // kept to undo a rejection
+                        v.term[r] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                         atomicAdd(&sh.ray_pts, npr);
                     }
                 }
                 __syncthreads();
                 STAMP(4);
-                // ========== phase F: chi^2 from the first changed ray on ==========
-                // terms in parallel into LDS, then ONE lane adds them in k order
-                // (MCsub.jl:170-172), 8 terms per LDS round trip
+            }
+            // ==== phase F: chi^2 + decision (tid 0) || next proposal, tile maxima (others) ====
+            if (tid == 0) {
+                double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
                 const int k0 = sh.k0;
-                double C = (tid == 0 && k0 > 0) ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
-                for (int base = k0; base < n; base += chi_chunk) {
-                    const int cnt = min(chi_chunk, n - base);
-                    for (int k = tid; k < cnt; k += kChainThreads) {
-                        const int r = base + k;
-                        const double pt = v.rflag[r] ? v.cptS[r] : v.ptS[r];
-                        const double df = pt - v.tS[r];
-                        const double sg = v.sig[r];
-                        v.chi[k] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
-                    }
-                    __syncthreads();
-                    if (tid == 0) {
-                        int k = 0;
-                        for (; k + 8 <= cnt; k += 8) {
-                            double t[8], c[8];
+                if (fwd) {
+                    // ONE lane adds the terms in k order (MCsub.jl:170-172); phase E put
+                    // the changed rays' new terms in place (the old ones wait in cterm)
+                    double C = k0 > 0 ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
+                    int k = k0;
+                    for (; k + 8 <= n; k += 8) {
+                        double t[8], c[8];
 #pragma unroll
-                            for (int u = 0; u < 8; ++u) t[u] = v.chi[k + u];
+                        for (int u = 0; u < 8; ++u) t[u] = v.term[k + u];
 #pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                C = C + t[u];
-                                c[u] = C;
-                            }
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) v.cprefix[base + k + u] = c[u];
+                        for (int u = 0; u < 8; ++u) {
+                            C = C + t[u];
+                            c[u] = C;
                         }
-                        for (; k < cnt; ++k) {
-                            C = C + v.chi[k];
-                            v.cprefix[base + k] = C;
-                        }
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) v.cprefix[k + u] = c[u];
                     }
-                    if (base + chi_chunk < n) __syncthreads();  // the LDS terms are reused
-                }
-                phi_n = k0 < n ? C : sh.phi;
-                if (tid == 0) {
+                    for (; k < n; ++k) {
+                        C = C + v.term[k];
+                        v.cprefix[k] = C;
+                    }
+                    phi_n = k0 < n ? C : sh.phi;
                     sh.evaluations += 1;
                     // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
                     // candidate points (coords + cached slot/distance, 36 B), grid queries
@@ -691,43 +731,63 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                                 (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
                                 (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28;
                 }
-            }
-            // ================= Metropolis-Hastings decision =================
-            if (tid == 0) {
-                const bool acc = tdchain::accept(P, pp, ncells, sh.phi, phi_n, czeta, sh.zeta_killed,
+                // Metropolis-Hastings decision
+                const bool acc = tdchain::accept(P, pp, ncells, sh.phi, phi_n, czeta, sh.cur.zeta_killed,
                                                  zetanew_death);
                 sh.accept = acc ? 1 : 0;
                 sh.phi_n = phi_n;
-                if (acc) sh.accepted[action] += 1;
+                if (acc) {
+                    sh.accepted[action] += 1;
+                    sh.g_op = action == tdchain::kBirth ? 2 : action == tdchain::kDeath ? 1
+                              : action == tdchain::kMove ? 3 : 0;
+                    sh.g_slot = action == tdchain::kBirth ? sh.cur.new_slot : slot_k;
+                    sh.g_ox = kx;
+                    sh.g_oy = ky;
+                    sh.g_oz = kz;
+                    sh.g_nx = pp.x;
+                    sh.g_ny = pp.y;
+                    sh.g_nz = pp.z;
+                }
+            } else if (tid == 64) {  // the next proposal as if this one were rejected
+                if (can_spec) {
+                    make_proposal(sh.spec, P, draws[(it + 1) & 63], ncells, sh.nfree, sh.nslots, d.free_slots, d.cx,
+                                  d.cy, d.cz, d.czeta, [&](int pos) { return v.ord[pos]; });
+                    sh.spec_ok = 1;
+                }
+            } else if (wv >= 2 && fwd && action != tdchain::kChange) {
+                // the hit tiles' maxima if the proposal is accepted (a tile = a DPP row)
+                const int nt = sh.n_tiles;
+                for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 128) {
+                    const int t = v.thit[i / kTilePts];
+                    const int q = v.tstart[t] + (i % kTilePts);
+                    unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
+                    if (q < v.tstart[t + 1]) {
+                        const double cd = d.cand_d[q], bd = d.best_d[q];
+                        mk = (unsigned long long)__double_as_longlong(d.cand_flag[q] ? cd : bd);
+                    }
+                    mk = row_max_u64(mk);
+                    if ((i % kTilePts) == kTilePts - 1) v.ctm[i / kTilePts] = __longlong_as_double((long long)mk);
+                }
             }
             __syncthreads();
             STAMP(5);
-            // ================= phase G: commit =================
+            // ================= phase G: commit (or undo) =================
+            const int nc = sh.n_changed, nr = sh.n_rays;
             if (sh.accept) {
-                const int nc = sh.n_changed, nr = sh.n_rays, nt = sh.n_tiles, k0 = sh.k0;
+                const int nt = sh.n_tiles, k0 = sh.k0;
                 for (int c = tid; c < nc; c += kChainThreads) {
                     const int q = d.changed[c];
                     d.best_s[q] = d.cand_s[q];
                     d.best_d[q] = d.cand_d[q];
                     d.zeta0[q] = d.cand_z[q];
+                    d.cand_flag[q] = 0;
                 }
-                // tile maxima of the new distances (changed points lie in hit tiles;
-                // the overlay reads the new value whether or not it is committed yet)
-                if (P.debug_prior != 1 && action != tdchain::kChange)
-                    for (int i = tid; i < nt * kTilePts; i += kChainThreads) {  // 16 lanes (a DPP row) per tile
-                        const int t = v.thit[i / kTilePts];
-                        const int q = v.tstart[t] + (i % kTilePts);
-                        unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
-                        if (q < v.tstart[t + 1]) {
-                            const double cd = d.cand_d[q], bd = d.best_d[q];
-                            mk = (unsigned long long)__double_as_longlong(d.cand_flag[q] ? cd : bd);
-                        }
-                        mk = row_max_u64(mk);  // a tile = one DPP row of 16 lanes
-                        if ((i % kTilePts) == kTilePts - 1) v.tmaxd[t] = __longlong_as_double((long long)mk);
-                    }
+                if (fwd && action != tdchain::kChange)
+                    for (int i = tid; i < nt; i += kChainThreads) v.tmaxd[v.thit[i]] = v.ctm[i];
                 for (int rr = tid; rr < nr; rr += kChainThreads) {
                     const int r = v.rhit[rr];
                     v.ptS[r] = v.cptS[r];
+                    v.rflag[r] = 0;
                 }
                 for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
                 if (action == tdchain::kDeath)  // deleteat!: positions after the killed one shift down
@@ -736,10 +796,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         v.ord[j - 1] = s;
                         d.rank[s] = j - 1;
                     }
+                if (wv == kWaves - 1 && sh.g_op) grid_apply(d, sh, lane);
                 if (tid == 0) {
-                    const int sk = sh.slot_k;
+                    const int sk = slot_k;
                     if (action == tdchain::kBirth) {  // append!
-                        const int s = sh.new_slot;
+                        const int s = sh.cur.new_slot;
                         d.cx[s] = pp.x;
                         d.cy[s] = pp.y;
                         d.cz[s] = pp.z;
@@ -751,48 +812,71 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         else
                             sh.nslots += 1;
                         sh.ncells = ncells + 1;
-                        sh.g_op = 2;
-                        sh.g_slot = s;
                     } else if (action == tdchain::kDeath) {
                         d.free_slots[sh.nfree] = sk;
                         sh.nfree += 1;
                         d.rank[sk] = -1;
                         sh.ncells = ncells - 1;
-                        sh.g_op = 1;
-                        sh.g_slot = sk;
                     } else if (action == tdchain::kChange) {
                         d.czeta[sk] = pp.zeta;
                     } else {
                         d.cx[sk] = pp.x;
                         d.cy[sk] = pp.y;
                         d.cz[sk] = pp.z;
-                        sh.g_op = 3;
-                        sh.g_slot = sk;
                     }
-                    sh.g_ox = sh.kx;
-                    sh.g_oy = sh.ky;
-                    sh.g_oz = sh.kz;
-                    sh.g_nx = pp.x;
-                    sh.g_ny = pp.y;
-                    sh.g_nz = pp.z;
                     sh.phi = sh.phi_n;
+                }
+            } else {  // rejected: flags down, the changed rays get their old chi^2 terms back
+                for (int c = tid; c < nc; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
+                for (int rr = tid; rr < nr; rr += kChainThreads) {
+                    const int r = v.rhit[rr];
+                    v.term[r] = v.cterm[r];
+                    v.rflag[r] = 0;
                 }
             }
         }
-        if (tid == 0) {
-            if (prof_on) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
-            sh.iter += 1;
-            sh.clr_changed = sh.n_changed;
-            sh.clr_rays = sh.n_rays;
+        // ===== end of iteration: the next proposal (wave 0; draws refilled every 64) =====
+        if (wv == 0) {
+            if (lane == 0) {
+                if (prof_on) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
+                sh.iter += 1;
+            }
+            if (it + 1 < iters) {
+                if (((it + 1) & 63) == 0) {
+                    wave_sync_lds();
+                    draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
+                    wave_sync_lds();
+                }
+                if (lane == 0) {
+                    const bool acc = sh.accept != 0;
+                    // the guess holds unless an accepted proposal changed what it read
+                    const bool keep = sh.spec_ok && can_spec &&
+                                      (!acc || ((action == tdchain::kChange || action == tdchain::kMove) &&
+                                                sh.spec.slot_k != slot_k));
+                    if (keep) {
+                        sh.cur = sh.spec;
+                    } else {
+                        // a just-killed position: later positions read the pre-shift order
+                        const int killed = (acc && action == tdchain::kDeath) ? (int)pp.index : -1;
+                        make_proposal(sh.cur, P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots, d.free_slots,
+                                      d.cx, d.cy, d.cz, d.czeta, [&](int pos) {
+                                          return (killed >= 0 && pos >= killed) ? d.order_tmp[pos + 1] : v.ord[pos];
+                                      });
+                    }
+                    if (sh.cur.p.active) sh.proposed[sh.cur.p.action] += 1;
+                    sh.spec_ok = 0;
+                    sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
+                    sh.pts_seen = sh.ray_pts = 0;
+                    sh.k0 = n;
+                    sh.accept = 0;
+                }
+            }
         }
         __syncthreads();
         STAMP(6);
     }
 
-    // ---- leave a clean state behind: flags, pending grid update, LDS copies ----
-    for (int c = tid; c < sh.clr_changed; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
-    for (int c = tid; c < sh.clr_rays; c += kChainThreads) v.rflag[v.rhit[c]] = 0;
-    if (wv == kWaves - 1 && sh.g_op) grid_apply(d, sh, lane);
+    // ---- leave the LDS copies behind (flags and grid are already clean) ----
     if constexpr (SMALL) {
         for (int i = tid; i < NT; i += kChainThreads) d.tile_maxd[i] = v.tmaxd[i];
         for (int i = tid; i < n; i += kChainThreads) {

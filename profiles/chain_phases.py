@@ -17,8 +17,8 @@ sys.path.insert(0, ROOT)
 import tonga  # noqa: E402
 
 # k_chain_run phases A..G (chain_kernels.hip, STAMP(0..6))
-PHASES = ["A draw + flags + grid update", "B tiles + birth/death query", "C points", "D orphans", "E ray sums",
-          "F chi2 + accept", "G commit"]
+PHASES = ["(loop top)", "B tiles + birth/death query", "C points", "D orphans", "E ray sums",
+          "F chi2 + accept || next proposal, tile maxima", "G commit + grid update + next proposal"]
 
 
 def main():
