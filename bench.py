@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--batch-chains", type=int, default=256,
                     help="size of the extra many-chains-per-GPU measurement on rank 0 (0 = skip)")
     ap.add_argument("--batch-iters", type=int, default=1000)
+    ap.add_argument("--no-stress", action="store_true",
+                    help="skip the config-5 stress block (10k synthetic rays x 20k cells)")
     return ap.parse_args()
 
 
@@ -200,6 +202,8 @@ def main():
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
     if rank == 0 and not a.no_full_evaluate:
         out["full_evaluate"] = full_evaluate(tt, ctx, model, N)
+    if rank == 0 and not a.no_stress:
+        out["stress"] = stress(tt)
     if rank == 0 and a.batch_chains > 0:
         out["many_chains"] = many_chains(tt, ctx, ds, prm, model, a.batch_chains, a.batch_iters)
     if rank == 0 and not a.no_cpu_baseline:
@@ -245,30 +249,61 @@ def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3):
 
 
 def full_evaluate(tt, ctx, model, N, reps=50):
+    """The drop-in td_evaluate (MCsub.jl:123-185) on the same model, both
+    nearest-cell methods: the bucket grid (default from 256 cells) and the
+    reference-shaped brute force (every point x every cell), whose dominant
+    kernel nn_partial is FP64-VALU bound (no FMA: 39.3 TFLOP/s roof)."""
     cells = model.cells()
-    for _ in range(3):
-        ctx.evaluate(cells)
-    ctx.timing(enable=True, reset=True)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        ctx.evaluate(cells)
-    el = (time.perf_counter() - t0) / reps
-    nl, nn_ms = ctx.timing(kernel="nn_partial")
-    _, mg_ms = ctx.timing(kernel="nn_merge")
-    _, rs_ms = ctx.timing(kernel="ray_sums")
-    _, c2_ms = ctx.timing(kernel="chi2")
-    ctx.timing(enable=False)
     E = ctx.P * N
-    t_nn = nn_ms / 1e3 / max(nl, 1)
+    out = {}
+    kernels = {"grid": ["nn_grid_build", "nn_grid", "nn_fallback", "ray_sums", "chi2"],
+               "brute_force": ["nn_partial", "nn_merge", "ray_sums", "chi2"]}
+    for name, method in (("grid", ctx.NN_GRID), ("brute_force", ctx.NN_BRUTE)):
+        ctx.set_nn_method(method)
+        for _ in range(3):
+            ctx.evaluate(cells)
+        ctx.timing(enable=True, reset=True)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ctx.evaluate(cells)
+        el = (time.perf_counter() - t0) / reps
+        km = {}
+        for k in kernels[name]:
+            nl, ms = ctx.timing(kernel=k)
+            km[k] = round(ms / max(nl, 1), 4)
+        ctx.timing(enable=False)
+        out[name] = {"evaluate_ms": round(el * 1e3, 4), "evaluates_per_s": round(1.0 / el, 1),
+                     "nn_pair_evals_per_s_equiv": round(E / el, 1), "kernel_ms": km}
+    ctx.set_nn_method(ctx.NN_AUTO)
+    t_nn = out["brute_force"]["kernel_ms"]["nn_partial"] / 1e3
     flops = 8.0 * E  # 3 sub + 3 mul + 2 add per distance, no FMA allowed
-    tf = flops / t_nn / 1e12
-    return {"evaluate_ms": round(el * 1e3, 4), "evaluates_per_s": round(1.0 / el, 1),
-            "nn_pair_evals_per_s": round(E / el, 1),
-            "kernel_ms": {"nn_partial": round(t_nn * 1e3, 4), "nn_merge": round(mg_ms / max(nl, 1), 4),
-                          "ray_sums": round(rs_ms / max(nl, 1), 4), "chi2": round(c2_ms / max(nl, 1), 4)},
-            "roofline": {"kernel": "nn_partial", "bound": "valu-fp64", "achieved": round(tf, 3),
-                         "peak": FP64_NOFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / FP64_NOFMA_PEAK_TFLOPS, 4),
-                         "flops_per_launch": flops}}
+    tf = flops / t_nn / 1e12 if t_nn > 0 else 0.0
+    out["brute_force"]["roofline"] = {"kernel": "nn_partial", "bound": "valu-fp64", "achieved": round(tf, 3),
+                                      "peak": FP64_NOFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                      "frac": round(tf / FP64_NOFMA_PEAK_TFLOPS, 4), "flops_per_launch": flops}
+    return out
+
+
+def stress(tt, chain_iters=2000):
+    """BASELINE config 5 on one GPU: 10k synthetic rays (seed 5) x 20k cells.
+    The drop-in evaluate with both nearest-cell methods, and the device chain
+    (its tiles / rays / order no longer fit in LDS: the HBM layout)."""
+    ds = tt.synthetic_rays(10000, seed=5)
+    ctx = tt.TdContext.from_datastruct(ds)
+    model = tt.random_model(20000, 5)
+    res = {"rays": int(ctx.n), "points": int(ctx.P), "cells": 20000}
+    res["evaluate"] = full_evaluate(tt, ctx, model, 20000, reps=5)
+    prm = tt.define_TDstructrure().replace(max_cells=40000)
+    ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=77, chain=1), model)
+    ch.run(200)
+    t0 = time.perf_counter()
+    ch.run(chain_iters)
+    el = time.perf_counter() - t0
+    res["chain"] = {"proposals_per_s": round(chain_iters / el, 1), "iters": chain_iters,
+                    "layout": "hbm (tiles, rays, order do not fit in LDS)"}
+    ch.close()
+    ctx.close()
+    return res
 
 
 def cpu_baseline(ds, model, seconds):

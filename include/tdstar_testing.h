@@ -39,6 +39,15 @@ int tdt_chain_profile(td_chain *ch, int enable, int64_t out[16]);
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);
 
+/* Device engine layout: 0 (default) mirrors tiles, rays and the Julia order
+ * in LDS when they fit (the 381-ray configs); 1 keeps them in HBM, the path
+ * larger geometries take.  Same results either way. */
+int tdt_chain_set_lds_mode(td_chain *ch, int mode);
+/* Nearest-cell method of td_evaluate / td_interpolate: 0 auto (bucket grid
+ * from 256 cells on), 1 brute force (every point x every cell), 2 bucket grid.
+ * All give the same answer (the lexicographic (distance, index) minimum). */
+int tdt_set_nn_method(td_ctx *ctx, int method);
+
 #ifdef __cplusplus
 }
 #endif

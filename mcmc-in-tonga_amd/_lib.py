@@ -75,6 +75,8 @@ SIGNATURES = {
     "tdt_draws": (None, [_u64, _u32, _u64, _pd]),
     "tdt_propose": (ctypes.c_int, [ctypes.POINTER(TdChainParams), _u64, _i64, _pd, _pd, _pd, _pd, _d, _pd]),
     "tdt_chain_profile": (ctypes.c_int, [_vp, ctypes.c_int, _pi64]),
+    "tdt_set_nn_method": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "tdt_chain_set_lds_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_accept": (ctypes.c_int, [ctypes.POINTER(TdChainParams), ctypes.c_int, _d, _d, _i64, _d, _d, _d, _d, _d]),
 }
 

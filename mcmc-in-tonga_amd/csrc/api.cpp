@@ -83,6 +83,41 @@ double likelihood_constant(const double *sig, int64_t n) {
     return julia_sum(t.data(), n);
 }
 
+CellGrid make_cell_grid(const double lo[3], const double hi[3], double target, int max_dim, int64_t max_buckets) {
+    double ext[3], prod = 1.0;
+    int k = 0;
+    for (int a = 0; a < 3; ++a) {
+        ext[a] = hi[a] > lo[a] ? hi[a] - lo[a] : 0.0;
+        if (ext[a] > 0.0) {
+            prod *= ext[a];
+            ++k;
+        }
+    }
+    int g[3] = {1, 1, 1};
+    if (k > 0 && target > 1.0) {
+        const double h = std::pow(prod / target, 1.0 / k);  // edge of a cubic bucket
+        for (int a = 0; a < 3; ++a)
+            if (ext[a] > 0.0) g[a] = (int)std::min<double>(max_dim, std::max(1.0, std::ceil(ext[a] / h)));
+        while ((int64_t)g[0] * g[1] * g[2] > max_buckets) {  // shrink the largest axis
+            int a = 0;
+            for (int b = 1; b < 3; ++b)
+                if (g[b] > g[a]) a = b;
+            g[a] = std::max(1, g[a] * 3 / 4);
+        }
+    }
+    CellGrid G{};
+    G.gx = g[0]; G.gy = g[1]; G.gz = g[2];
+    G.x0 = lo[0]; G.y0 = lo[1]; G.z0 = lo[2];
+    double *inv[3] = {&G.ix, &G.iy, &G.iz}, *h[3] = {&G.hx, &G.hy, &G.hz}, *e[3] = {&G.ex, &G.ey, &G.ez};
+    for (int a = 0; a < 3; ++a) {
+        *inv[a] = ext[a] > 0.0 ? g[a] / ext[a] : 0.0;
+        *h[a] = ext[a] > 0.0 ? ext[a] / g[a] : 0.0;
+        // floor((v - v0) * inv) vs v0 + i*h: a few ulps of the box's magnitude
+        *e[a] = std::ldexp(std::fabs(lo[a]) + std::fabs(hi[a]) + ext[a], -44);
+    }
+    return G;
+}
+
 int ensure_cells(td_ctx *ctx, int64_t ncells) {
     if (ncells <= ctx->cell_cap && ctx->cells) return TD_OK;
     int64_t cap = ctx->cell_cap > 0 ? ctx->cell_cap : 256;
@@ -109,11 +144,36 @@ int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z,
     std::memcpy(h + s, y, sizeof(double) * (size_t)ncells);
     std::memcpy(h + 2 * s, z, sizeof(double) * (size_t)ncells);
     std::memcpy(h + 3 * s, zeta, sizeof(double) * (size_t)ncells);
+    const double *src[3] = {x, y, z};
+    for (int a = 0; a < 3; ++a) {  // box of the cells for the bucket grid
+        double lo = HUGE_VAL, hi = -HUGE_VAL;
+        for (int64_t i = 0; i < ncells; ++i) {
+            const double v = src[a][i];
+            lo = v < lo ? v : lo;  // NaN compares false: skipped
+            hi = v > hi ? v : hi;
+        }
+        ctx->cell_lo[a] = lo <= hi ? lo : 0.0;
+        ctx->cell_hi[a] = lo <= hi ? hi : 0.0;
+    }
     // four slices of the SoA (one copy if the set fills the capacity)
     for (int k = 0; k < 4; ++k)
         TD_HIP(ctx, hipMemcpyAsync(ctx->cells + k * s, h + k * s, sizeof(double) * (size_t)ncells,
                                    hipMemcpyHostToDevice, ctx->stream));
     return TD_OK;
+}
+
+hipError_t nearest_uploaded(td_ctx *ctx, const double *qx, const double *qy, const double *qz, int64_t npts,
+                            int64_t qy_stride, int64_t qz_stride, int64_t ncells, int *best_i, double *best_d,
+                            double *zeta0) {
+    Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
+    const bool grid = ctx->nn_method == 2 || (ctx->nn_method == 0 && ncells >= kGridMinCells);
+    if (grid && ncells > 0) {
+        const CellGrid G = make_cell_grid(ctx->cell_lo, ctx->cell_hi, (double)ncells / 2.0, 4096, kGridMaxBuckets);
+        return launch_nearest_grid(qx, qy, qz, npts, qy_stride, qz_stride, ctx->cells, ctx->cell_cap, ncells, G,
+                                   ctx->nn, ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm);
+    }
+    return launch_nearest(qx, qy, qz, npts, qy_stride, qz_stride, ctx->cells, ctx->cell_cap, ncells, ctx->nn,
+                          ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm);
 }
 
 }  // namespace tdstar
@@ -128,7 +188,7 @@ void free_ctx(td_ctx *c) {
     c->timer.release();
     void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->cells,
                    c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->ptS, c->phi,
-                   c->q, c->q_i, c->q_z, c->chain_desc};
+                   c->q, c->q_i, c->q_z, c->chain_desc, c->nn.g_count, c->nn.g_ent, c->nn.g_fb};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     void *host[] = {c->h_cells, c->h_out, c->h_best_i, c->h_q, c->h_q_i, c->h_q_z, c->h_chain_desc};
@@ -312,8 +372,7 @@ int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const dou
     if (rc) return rc;
     const auto &g = ctx->g;
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
-    hipError_t e = launch_nearest(g.px, g.py, g.pz, g.P, 1, 1, ctx->cells, ctx->cell_cap, nCells, ctx->nn,
-                                  ctx->num_cus, ctx->best_i, ctx->best_d, ctx->zeta0, ctx->stream, tm);
+    hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, nCells, ctx->best_i, ctx->best_d, ctx->zeta0);
     if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
     e = launch_ray_sums(g, ctx->zeta0, ctx->ptS, ctx->stream, tm);
     if (e != hipSuccess) return hip_err(ctx, e, "ray-sum kernel");
@@ -392,9 +451,8 @@ int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const 
     TD_HIP(ctx, hipMemcpyAsync(ctx->q, ctx->h_q, sizeof(double) * 3 * (size_t)qc, hipMemcpyHostToDevice, ctx->stream));
     int rc = upload_cells(ctx, xCell, yCell, zCell, zeta, nCells);
     if (rc) return rc;
-    hipError_t e = launch_nearest(ctx->q, ctx->q + qc, ctx->q + 2 * qc, np, ny == 1 ? 0 : 1, nz == 1 ? 0 : 1,
-                                  ctx->cells, ctx->cell_cap, nCells, ctx->nn, ctx->num_cus, ctx->q_i, nullptr,
-                                  ctx->q_z, ctx->stream, ctx->timer.on ? &ctx->timer : nullptr);
+    hipError_t e = nearest_uploaded(ctx, ctx->q, ctx->q + qc, ctx->q + 2 * qc, np, ny == 1 ? 0 : 1,
+                                    nz == 1 ? 0 : 1, nCells, ctx->q_i, nullptr, ctx->q_z);
     if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
     TD_HIP(ctx, hipMemcpyAsync(ctx->h_q_z, ctx->q_z, sizeof(double) * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
     if (nearest_out)
@@ -402,6 +460,12 @@ int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const 
     TD_HIP(ctx, hipStreamSynchronize(ctx->stream));
     std::memcpy(zeta_out, ctx->h_q_z, sizeof(double) * (size_t)np);
     if (nearest_out) std::memcpy(nearest_out, ctx->h_q_i, sizeof(int) * (size_t)np);
+    return TD_OK;
+}
+
+int tdt_set_nn_method(td_ctx *ctx, int method) {
+    if (!ctx || method < 0 || method > 2) return TD_ERR_ARG;
+    ctx->nn_method = method;
     return TD_OK;
 }
 

@@ -201,18 +201,8 @@ int device_setup(td_chain *ch) {
     ch->tile_start_host = tstart;
     const int cap = std::max<int>(ch->prm.max_cells, (int)ch->x.size()) + 1;
     // ---- bucket grid over the cells: ~2 cells per bucket at the starting size ----
-    CellGrid G{};
-    {
-        const double ex = ch->P.xmax - ch->P.xmin, ey = ch->P.ymax - ch->P.ymin, ez = ch->P.zmax - ch->P.zmin;
-        const double vol = std::max(ex, 1e-6) * std::max(ey, 1e-6) * std::max(ez, 1e-6);
-        const double nref = std::max<double>((double)ch->x.size(), 16.0);
-        const double h = std::cbrt(vol / std::max(1.0, nref / 2.0));
-        auto dim = [&](double e) { return e > 0.0 ? (int)std::min(256.0, std::max(1.0, std::ceil(e / h))) : 1; };
-        G.gx = dim(ex); G.gy = dim(ey); G.gz = dim(ez);
-        G.x0 = ch->P.xmin; G.y0 = ch->P.ymin; G.z0 = ch->P.zmin;
-        G.ix = ex > 0.0 ? G.gx / ex : 0.0; G.iy = ey > 0.0 ? G.gy / ey : 0.0; G.iz = ez > 0.0 ? G.gz / ez : 0.0;
-        G.hx = ex > 0.0 ? ex / G.gx : 0.0; G.hy = ey > 0.0 ? ey / G.gy : 0.0; G.hz = ez > 0.0 ? ez / G.gz : 0.0;
-    }
+    const double glo[3] = {ch->P.xmin, ch->P.ymin, ch->P.zmin}, ghi[3] = {ch->P.xmax, ch->P.ymax, ch->P.zmax};
+    const CellGrid G = make_cell_grid(glo, ghi, std::max<double>((double)ch->x.size(), 16.0) / 2.0, 256, 1 << 24);
     const size_t nbuckets = (size_t)G.gx * G.gy * G.gz;
     std::vector<int> bcount(nbuckets, 0);
     std::vector<BucketEntry> bent(nbuckets * kBucketCap, BucketEntry{0.0, 0.0, 0.0, 0, 0});
@@ -576,6 +566,12 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
     std::memcpy(out, v, sizeof v);
     return 0;
 }
+int tdt_chain_set_lds_mode(td_chain *ch, int mode) {
+    if (!ch || ch->engine != TD_ENGINE_DEVICE || mode < 0 || mode > 1) return TD_ERR_ARG;
+    ch->dev.lds_mode = mode;
+    return TD_OK;
+}
+
 int tdt_chain_profile(td_chain *ch, int enable, int64_t out[16]) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE) return TD_ERR_ARG;
     ch->dev.profile = enable;

@@ -43,31 +43,6 @@ struct ChainScalars {
     int pad;
 };
 
-// Bucket of a coordinate: clamp(floor((v - v0) * inv), 0, g - 1).  Cells
-// outside the box land in the boundary buckets, so "no bucket beyond" really
-// means no cell beyond.  Same function on host (build) and device (updates).
-struct CellGrid {
-    int gx, gy, gz;
-    double x0, y0, z0;
-    double ix, iy, iz;  // buckets per km
-    double hx, hy, hz;  // km per bucket
-};
-
-struct BucketEntry {
-    double x, y, z;
-    int slot, pad;
-};
-
-__host__ __device__ inline int grid_axis(double v, double v0, double inv, int g) {
-    const double f = (v - v0) * inv;
-    return f >= 0.0 ? (f < (double)g ? (int)f : g - 1) : 0;  // NaN -> 0
-}
-
-__host__ __device__ inline int grid_bucket(const CellGrid &G, double x, double y, double z) {
-    return (grid_axis(z, G.z0, G.iz, G.gz) * G.gy + grid_axis(y, G.y0, G.iy, G.gy)) * G.gx +
-           grid_axis(x, G.x0, G.ix, G.gx);
-}
-
 struct DevChain {
     // geometry (owned by the td_ctx)
     const double *px, *py, *pz, *w, *tS, *sig;
@@ -101,6 +76,7 @@ struct DevChain {
     uint64_t seed;
     uint32_t chain;
     int profile;  // diagnostic phase stamps (s_memtime) -- off in measured runs
+    int lds_mode;  // 0: mirror tiles/rays/order in LDS when they fit; 1: always work from HBM (testing)
     // uniform bucket grid over the cells
     CellGrid grid;
     int *bucket_count;      // [G]

@@ -34,6 +34,7 @@
 #include "chain_dev.h"
 #include "internal.h"
 #include "ray_sum.h"
+#include "wave_ops.h"
 
 namespace tdstar {
 
@@ -64,47 +65,6 @@ __device__ __forceinline__ double dist2(double cx, double cy, double cz, double 
 // 1e9 sentinel strictly (MCsub.jl:250,255).
 __device__ __forceinline__ bool better(double d, int r, double bd, int br) {
     return d < bd || (d == bd && d < kSentinel && r < br);
-}
-
-// ---- cross-lane reductions on 64-bit keys through DPP (VALU, no LDS) ----
-// A non-negative double orders like its bit pattern, so distances reduce as
-// unsigned 64-bit keys.  update_dpp returns `old` in lanes whose source is out
-// of the row or masked off, so `old` is the identity of the reduction.
-template <int CTRL, int RM>
-__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v, unsigned long long idn) {
-    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)idn, (int)(unsigned)v, CTRL, RM, 0xf, false);
-    const int hi =
-        __builtin_amdgcn_update_dpp((int)(unsigned)(idn >> 32), (int)(unsigned)(v >> 32), CTRL, RM, 0xf, false);
-    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-}
-__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
-__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
-// min over the 64 lanes of the wave, returned to every lane
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-    constexpr unsigned long long I = ~0ull;
-    v = umin64(v, dpp_u64<0x111, 0xf>(v, I));  // row_shr:1
-    v = umin64(v, dpp_u64<0x112, 0xf>(v, I));  // row_shr:2
-    v = umin64(v, dpp_u64<0x114, 0xf>(v, I));  // row_shr:4
-    v = umin64(v, dpp_u64<0x118, 0xf>(v, I));  // row_shr:8  -> lane 15 of a row: row min
-    v = umin64(v, dpp_u64<0x142, 0xa>(v, I));  // row_bcast:15 into rows 1, 3
-    v = umin64(v, dpp_u64<0x143, 0xc>(v, I));  // row_bcast:31 into rows 2, 3 -> lane 63: min
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
-    return ((unsigned long long)hi << 32) | lo;
-}
-// max over each row of 16 lanes, valid in the row's last lane (lane % 16 == 15)
-__device__ __forceinline__ unsigned long long row_max_u64(unsigned long long v) {
-    v = umax64(v, dpp_u64<0x111, 0xf>(v, 0ull));
-    v = umax64(v, dpp_u64<0x112, 0xf>(v, 0ull));
-    v = umax64(v, dpp_u64<0x114, 0xf>(v, 0ull));
-    v = umax64(v, dpp_u64<0x118, 0xf>(v, 0ull));
-    return v;
-}
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 struct OverlayZeta {
@@ -356,24 +316,9 @@ __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf,
     const bool any_over = __ballot(overfull) != 0ull;
     res.s = found ? __builtin_amdgcn_readlane(bs, win) : -1;
     res.z = found ? readlane_f64(bz, win) : 0.0;
-    // squared distance to the nearest outer face of the searched block
-    double lb = __builtin_huge_val();
-    auto face = [&lb](double v, double v0, double inv, double h, int g) {
-        const int i = grid_axis(v, v0, inv, g);
-        if (i - 1 > 0) {
-            const double gap = v - (v0 + (double)(i - 1) * h);
-            lb = gap > 0.0 ? fmin(lb, gap * gap) : 0.0;
-        }
-        if (i + 1 < g - 1) {
-            const double gap = (v0 + (double)(i + 2) * h) - v;
-            lb = gap > 0.0 ? fmin(lb, gap * gap) : 0.0;
-        }
-    };
-    face(x, G.x0, G.ix, G.hx, G.gx);
-    face(y, G.y0, G.iy, G.hy, G.gy);
-    face(z, G.z0, G.iz, G.hz, G.gz);
-    // the relative margin covers the rounding of bucket indices vs faces
-    res.proven = !ovf && !tied && !any_over && res.d < lb * (1.0 - 1e-9);
+    // every cell outside the 3x3x3 block is at least sqrt(lb) away
+    const double lb = grid_block_lb(G, x, y, z, 1);
+    res.proven = !ovf && !tied && !any_over && res.d < lb;
     return res;
 }
 
@@ -974,12 +919,14 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
     // one LDS size for the whole grid: the largest plan of any chain; the
     // small (LDS-mirrored) variant only if every chain fits
     size_t small = 0, big = 0;
+    bool force_hbm = false;
     for (int b = 0; b < nchains; ++b) {
         const DevChain &d = host[b];
         small = std::max(small, lds_plan(d.ntiles, d.n, d.cap, true).total);
         big = std::max(big, lds_plan(d.ntiles, d.n, d.cap, false).total);
+        force_hbm = force_hbm || d.lds_mode == 1;
     }
-    if (small <= kLdsBudget) {
+    if (small <= kLdsBudget && !force_hbm) {
         hipError_t e = hipFuncSetAttribute((const void *)k_chain_run<true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)small);
         if (e != hipSuccess) return e;

@@ -44,6 +44,8 @@ struct td_ctx {
     double *h_q_z = nullptr;
 
     tdstar::Timer timer;                // per-kernel HIP-event timing (td_timing_*)
+    double cell_lo[3] = {0, 0, 0}, cell_hi[3] = {0, 0, 0};  // box of the uploaded cells (NaN skipped)
+    int nn_method = 0;                  // 0 auto, 1 brute force, 2 bucket grid (tdt_set_nn_method)
     void *chain_desc = nullptr;         // device array of chain descriptors (td_chain_run_batch)
     size_t chain_desc_bytes = 0;
     void *h_chain_desc = nullptr;       // pinned staging of the same
@@ -67,6 +69,11 @@ int ensure_cells(td_ctx *ctx, int64_t ncells);
 // Pack cells into the pinned staging buffer and upload them (async on ctx->stream).
 int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                  int64_t ncells);
+// Nearest cell of npts query points against the uploaded cells (brute force
+// for small models, the bucket grid otherwise; same answer either way).
+hipError_t nearest_uploaded(td_ctx *ctx, const double *qx, const double *qy, const double *qz, int64_t npts,
+                            int64_t qy_stride, int64_t qz_stride, int64_t ncells, int *best_i, double *best_d,
+                            double *zeta0);
 // Julia Base.sum association (see oracle/README.md); used for the likelihood constant.
 double julia_sum(const double *a, int64_t n);
 double likelihood_constant(const double *sig, int64_t n);

@@ -38,11 +38,75 @@ struct Timer {
     void release();
 };
 
-// Workspace for the split-cells nearest search.
+// Bucket of a coordinate: clamp(floor((v - v0) * inv), 0, g - 1).  Cells
+// outside the box land in the boundary buckets, so "no bucket beyond" really
+// means no cell beyond.  Same function on host (build) and device (updates).
+struct CellGrid {
+    int gx, gy, gz;
+    double x0, y0, z0;
+    double ix, iy, iz;  // buckets per km
+    double hx, hy, hz;  // km per bucket
+    // allowance for the rounding of bucket assignment against the faces
+    // x0 + i*hx: a cell can sit up to ex on the wrong side of a face
+    double ex, ey, ez;
+};
+
+// A uniform grid with about `target` buckets over the box [lo, hi] (degenerate
+// axes get one bucket), at most `max_buckets` in all.
+CellGrid make_cell_grid(const double lo[3], const double hi[3], double target, int max_dim, int64_t max_buckets);
+
+struct BucketEntry {
+    double x, y, z;
+    int slot, pad;
+};
+
+__host__ __device__ inline int grid_axis(double v, double v0, double inv, int g) {
+    const double f = (v - v0) * inv;
+    return f >= 0.0 ? (f < (double)g ? (int)f : g - 1) : 0;  // NaN -> 0
+}
+
+__host__ __device__ inline int grid_bucket(const CellGrid &G, double x, double y, double z) {
+    return (grid_axis(z, G.z0, G.iz, G.gz) * G.gy + grid_axis(y, G.y0, G.iy, G.gy)) * G.gx +
+           grid_axis(x, G.x0, G.ix, G.gx);
+}
+
+// Squared distance from (x,y,z) in bucket column (i,j,k) to the nearest outer
+// face of the block of buckets [i-R, i+R] x [j-R, j+R] x [k-R, k+R], faces on
+// the grid boundary excluded (no cell lies beyond them).  Every cell outside
+// the block is at least this far away (0 when unknown; +inf when the block
+// covers the grid).
+__host__ __device__ inline double grid_block_lb(const CellGrid &G, double x, double y, double z, int R) {
+    double lb = __builtin_huge_val();
+    auto face = [&lb](double v, double v0, double inv, double h, double e, int g, int R_) {
+        const int i = grid_axis(v, v0, inv, g);
+        if (i - R_ > 0) {
+            const double gap = (v - (v0 + (double)(i - R_) * h)) - e;
+            lb = gap > 0.0 ? (gap * gap < lb ? gap * gap : lb) : 0.0;
+        }
+        if (i + R_ < g - 1) {
+            const double gap = ((v0 + (double)(i + R_ + 1) * h) - v) - e;
+            lb = gap > 0.0 ? (gap * gap < lb ? gap * gap : lb) : 0.0;
+        }
+    };
+    face(x, G.x0, G.ix, G.hx, G.ex, G.gx, R);
+    face(y, G.y0, G.iy, G.hy, G.ey, G.gy, R);
+    face(z, G.z0, G.iz, G.hz, G.ez, G.gz, R);
+    return lb;
+}
+
+constexpr int kGridMaxBuckets = 1 << 16;  // bucket grid of the evaluate path
+constexpr int kGridCap = 16;               // entries per bucket (a fuller bucket is searched by brute force)
+constexpr int kGridMinCells = 256;     // below: the brute force is as fast
+
+// Workspace for the nearest searches (split brute force; bucket grid).
 struct NNWork {
     double *part_d = nullptr;  // [chunks][npts]
     int *part_i = nullptr;
     size_t cap = 0;            // elements
+    int *g_count = nullptr;        // [buckets] cells per bucket
+    BucketEntry *g_ent = nullptr;  // [buckets][kGridCap] entries {x, y, z, cell index}
+    int *g_fb = nullptr;           // [npts] points left to the brute force, then their count
+    size_t g_count_cap = 0, g_ent_cap = 0, g_fb_cap = 0;  // bytes
 };
 
 struct Geometry {
@@ -69,6 +133,14 @@ hipError_t launch_nearest(const double *qx, const double *qy, const double *qz, 
                           int64_t qy_stride, int64_t qz_stride, const double *cells, int64_t stride,
                           int64_t ncells, NNWork &work, int num_cus, int *best_i, double *best_d,
                           double *zeta0, hipStream_t s, Timer *tm = nullptr);
+
+// Same result as launch_nearest through a bucket grid G over the cells (which
+// must all lie in G's box; G.gx*G.gy*G.gz <= kGridMaxBuckets, ncells >= 1).
+// Cells are ordered by nothing but their index: ties resolve exactly.
+hipError_t launch_nearest_grid(const double *qx, const double *qy, const double *qz, int64_t npts,
+                               int64_t qy_stride, int64_t qz_stride, const double *cells, int64_t stride,
+                               int64_t ncells, const CellGrid &G, NNWork &work, int num_cus, int *best_i,
+                               double *best_d, double *zeta0, hipStream_t s, Timer *tm = nullptr);
 
 // ptS[i] = julia_sum_j w[j] * ((0.5*(z0[j]+z0[j+1])) / 1000) per ray (MCsub.jl:147-159).
 hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm = nullptr);

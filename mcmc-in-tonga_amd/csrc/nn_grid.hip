@@ -1,0 +1,215 @@
+// nn_grid.hip -- nearest cell of many query points through a uniform bucket
+// grid over the cells: the drop-in evaluate / Interpolation path for larger
+// models (v_nearest, MCsub.jl:247-263, for every ray point).
+//
+// The answer is the reference's: the lexicographic minimum of (squared
+// distance, cell index) over all cells, among distances below the 1e9
+// sentinel -- v_nearest's strict '<' scan in index order keeps the FIRST
+// minimum.  The grid only decides where to look:
+//   k_grid_fill    one lane per cell: append {x, y, z, index} to its bucket
+//                  (kGridCap entries; a fuller bucket is flagged);
+//   k_nn_grid      32 lanes per point, one per bucket of the 3x3x3 block
+//                  around it, DPP reduction; the answer counts only if it is
+//                  strictly closer than every face of the block
+//                  (grid_block_lb), i.e. than every cell outside, and no
+//                  bucket of the block overflowed -- else the point goes on a
+//                  list;
+//   k_nn_fallback  one wave per listed point: all cells (brute force).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+
+#include "internal.h"
+#include "wave_ops.h"
+
+namespace tdstar {
+
+namespace {
+
+__device__ __forceinline__ double dist2_q(double cx, double cy, double cz, double x, double y, double z) {
+    // (mx-x)^2 + (my-y)^2 + (mz-z)^2, MCsub.jl:254, left to right, unfused
+    const double dx = cx - x, dy = cy - y, dz = cz - z;
+    double d = dx * dx;
+    d = d + dy * dy;
+    d = d + dz * dz;
+    return d;
+}
+
+// lexicographic (distance, index) update; distances >= the sentinel never count
+__device__ __forceinline__ void take(double d, int i, double &bd, int &bi) {
+    if (d < bd || (d == bd && d < kSentinel && i < bi)) {
+        bd = d;
+        bi = i;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_grid_fill(const double *__restrict__ cells, int stride, int ncells,
+                                                   CellGrid G, int *__restrict__ count,
+                                                   BucketEntry *__restrict__ ent, int *__restrict__ fb_count) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *fb_count = 0;  // the fallback list of this search starts empty
+    if (i >= ncells) return;
+    const double x = cells[i], y = cells[stride + i], z = cells[2 * stride + i];
+    const int b = grid_bucket(G, x, y, z);
+    const int pos = atomicAdd(&count[b], 1);  // order inside a bucket does not matter
+    if (pos < kGridCap) ent[(long)b * kGridCap + pos] = BucketEntry{x, y, z, i, 0};
+}
+
+// lexicographic min of (d, i) over each half-wave (32 lanes), to every lane
+__device__ __forceinline__ void half_min(double &d, int &i) {
+    unsigned long long k = (unsigned long long)__double_as_longlong(d);
+    constexpr unsigned long long I = ~0ull;
+    k = umin64(k, dpp_u64<0x111, 0xf>(k, I));
+    k = umin64(k, dpp_u64<0x112, 0xf>(k, I));
+    k = umin64(k, dpp_u64<0x114, 0xf>(k, I));
+    k = umin64(k, dpp_u64<0x118, 0xf>(k, I));
+    k = umin64(k, dpp_u64<0x142, 0xa>(k, I));  // row_bcast:15 -> lanes 31, 63: half minima
+    const int src = (threadIdx.x & 32) | 31;
+    const unsigned long long km = (unsigned long long)__shfl(k, src, 64);
+    const bool at = (unsigned long long)__double_as_longlong(d) == km;
+    unsigned long long r = at ? (unsigned long long)(unsigned)i : I;
+    r = umin64(r, dpp_u64<0x111, 0xf>(r, I));
+    r = umin64(r, dpp_u64<0x112, 0xf>(r, I));
+    r = umin64(r, dpp_u64<0x114, 0xf>(r, I));
+    r = umin64(r, dpp_u64<0x118, 0xf>(r, I));
+    r = umin64(r, dpp_u64<0x142, 0xa>(r, I));
+    const unsigned long long rm = (unsigned long long)__shfl(r, src, 64);
+    d = __longlong_as_double((long long)km);
+    i = rm == I ? INT_MAX : (int)rm;
+}
+
+__global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, const double *__restrict__ qy,
+                                                 const double *__restrict__ qz, int npts, int ys, int zs, CellGrid G,
+                                                 const int *__restrict__ count, const BucketEntry *__restrict__ ent,
+                                                 const double *__restrict__ zeta_cells, int *__restrict__ best_i,
+                                                 double *__restrict__ best_d, double *__restrict__ zeta0,
+                                                 int *__restrict__ fb_list, int *__restrict__ fb_count) {
+    const int hl = threadIdx.x & 31;                             // lane in the half-wave
+    const int p = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;  // one point per half-wave
+    const int pc = min(p, npts - 1);                              // whole half-waves stay for the DPP
+    const double x = qx[pc], y = qy[(long)pc * ys], z = qz[(long)pc * zs];
+    const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
+              bk = grid_axis(z, G.z0, G.iz, G.gz);
+    // the 3x3x3 block (one bucket per lane), then the 5x5x5 one (four per lane)
+    for (int R = 1; R <= 2; ++R) {
+        const int W = 2 * R + 1, nbk = W * W * W;
+        double bd = kSentinel;
+        int bx = INT_MAX;
+        bool over = false;
+        for (int t = hl; t < nbk; t += 32) {
+            const int ii = bi + t % W - R, jj = bj + (t / W) % W - R, kk = bk + t / (W * W) - R;
+            const bool inb = ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
+            const long b = inb ? ((long)kk * G.gy + jj) * G.gx + ii : 0;
+            // one round of loads: the count and the first two entries
+            const int cnt = inb ? count[b] : 0;
+            const BucketEntry e0 = ent[b * kGridCap], e1 = ent[b * kGridCap + 1];
+            if (cnt > 0) take(dist2_q(e0.x, e0.y, e0.z, x, y, z), e0.slot, bd, bx);
+            if (cnt > 1) take(dist2_q(e1.x, e1.y, e1.z, x, y, z), e1.slot, bd, bx);
+            for (int k = 2; k < min(cnt, kGridCap); ++k) {
+                const BucketEntry e = ent[b * kGridCap + k];
+                take(dist2_q(e.x, e.y, e.z, x, y, z), e.slot, bd, bx);
+            }
+            over = over || cnt > kGridCap;
+        }
+        half_min(bd, bx);
+        const unsigned long long ov = __ballot(over);
+        const bool any_over = ((ov >> (threadIdx.x & 32)) & 0xffffffffull) != 0ull;
+        if (!any_over && bd < grid_block_lb(G, x, y, z, R)) {  // nothing outside can tie or win
+            if (hl == 0 && p < npts) {
+                const bool found = bd < kSentinel;
+                best_i[p] = found ? bx : -1;
+                if (best_d) best_d[p] = bd;
+                if (zeta0) zeta0[p] = found ? zeta_cells[bx] : 0.0;  // MCsub.jl:249
+            }
+            return;  // the whole half-wave: its point is answered
+        }
+    }
+    if (hl == 0 && p < npts) fb_list[atomicAdd(fb_count, 1)] = p;
+}
+
+// One wave per listed point: every cell, lexicographic min over the lanes.
+__global__ __launch_bounds__(256) void k_nn_fallback(const double *__restrict__ qx, const double *__restrict__ qy,
+                                                     const double *__restrict__ qz, int ys, int zs,
+                                                     const int *__restrict__ fb_list, const int *__restrict__ fb_count,
+                                                     const double *__restrict__ cells, int stride, int ncells,
+                                                     int *__restrict__ best_i, double *__restrict__ best_d,
+                                                     double *__restrict__ zeta0, int *__restrict__ count, int nb) {
+    // the bucket counts are spent: leave them zero for the next search
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x) count[b] = 0;
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * (blockDim.x / 64);
+    const int nfb = *fb_count;
+    for (int f = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); f < nfb; f += nwaves) {
+        const int p = fb_list[f];
+        const double x = qx[p], y = qy[(long)p * ys], z = qz[(long)p * zs];
+        double bd = kSentinel;
+        int bx = INT_MAX;
+        int j = lane;
+        for (; j + 64 < ncells; j += 128) {  // two cells per round
+            const double ax = cells[j], ay = cells[stride + j], az = cells[2 * stride + j];
+            const double cx = cells[j + 64], cy = cells[stride + j + 64], cz = cells[2 * stride + j + 64];
+            take(dist2_q(ax, ay, az, x, y, z), j, bd, bx);
+            take(dist2_q(cx, cy, cz, x, y, z), j + 64, bd, bx);
+        }
+        if (j < ncells) take(dist2_q(cells[j], cells[stride + j], cells[2 * stride + j], x, y, z), j, bd, bx);
+        const unsigned long long kd = wave_min_u64((unsigned long long)__double_as_longlong(bd));
+        const bool at = (unsigned long long)__double_as_longlong(bd) == kd;
+        const unsigned long long ki = wave_min_u64(at ? (unsigned long long)(unsigned)bx : ~0ull);
+        if (lane == 0) {
+            const double d = __longlong_as_double((long long)kd);
+            const int i = (d < kSentinel && ki != ~0ull) ? (int)ki : -1;
+            best_i[p] = i;
+            if (best_d) best_d[p] = d;
+            if (zeta0) zeta0[p] = i >= 0 ? cells[3 * stride + i] : 0.0;  // MCsub.jl:249
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_nearest_grid(const double *qx, const double *qy, const double *qz, int64_t npts,
+                               int64_t qy_stride, int64_t qz_stride, const double *cells, int64_t stride,
+                               int64_t ncells, const CellGrid &G, NNWork &work, int num_cus, int *best_i,
+                               double *best_d, double *zeta0, hipStream_t s, Timer *tm) {
+    if (npts <= 0) return hipSuccess;
+    const int64_t nb = (int64_t)G.gx * G.gy * G.gz;
+    if (nb > kGridMaxBuckets || ncells <= 0) return hipErrorInvalidValue;
+    hipError_t e = hipSuccess;
+    auto grow = [&e](void *&ptr, size_t &cap, size_t need) {
+        if (e != hipSuccess || need <= cap) return;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+        e = hipMalloc(&ptr, need);
+        if (e == hipSuccess) cap = need;
+    };
+    const size_t had = work.g_count_cap;
+    grow(reinterpret_cast<void *&>(work.g_count), work.g_count_cap, sizeof(int) * (size_t)nb);
+    if (e == hipSuccess && work.g_count_cap != had)  // fresh counters start at zero; later ones are
+        e = hipMemsetAsync(work.g_count, 0, work.g_count_cap, s);  // left zero by k_nn_fallback
+    grow(reinterpret_cast<void *&>(work.g_ent), work.g_ent_cap, sizeof(BucketEntry) * (size_t)nb * kGridCap);
+    grow(reinterpret_cast<void *&>(work.g_fb), work.g_fb_cap, sizeof(int) * (size_t)(npts + 1));
+    if (e != hipSuccess) return e;
+    int *fb_count = work.g_fb + npts;
+    hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
+    hipLaunchKernelGGL(k_grid_fill, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, s, cells, (int)stride,
+                       (int)ncells, G, work.g_count, work.g_ent, fb_count);
+    if (tm) tm->end("nn_grid_build", t0, s);
+    hipEvent_t t1 = tm ? tm->begin(s) : nullptr;
+    hipLaunchKernelGGL(k_nn_grid, dim3((unsigned)((npts + 7) / 8)), dim3(256), 0, s, qx, qy, qz, (int)npts,
+                       (int)qy_stride, (int)qz_stride, G, work.g_count, work.g_ent, cells + 3 * stride, best_i,
+                       best_d, zeta0, work.g_fb, fb_count);
+    if (tm) tm->end("nn_grid", t1, s);
+    hipEvent_t t2 = tm ? tm->begin(s) : nullptr;
+    const int blocks = std::max(1, std::min<int>(num_cus * 2, (int)((npts + 3) / 4)));
+    hipLaunchKernelGGL(k_nn_fallback, dim3(blocks), dim3(256), 0, s, qx, qy, qz, (int)qy_stride, (int)qz_stride,
+                       work.g_fb, fb_count, cells, (int)stride, (int)ncells, best_i, best_d, zeta0, work.g_count,
+                       (int)nb);
+    if (tm) tm->end("nn_fallback", t2, s);
+    return hipGetLastError();
+}
+
+}  // namespace tdstar

@@ -1,0 +1,51 @@
+// wave_ops.h -- cross-lane reductions for one 64-lane wave on gfx950, through
+// DPP (row_shr / row_bcast VALU modifiers) instead of LDS permutes: a 6-step
+// ds_bpermute reduction of a double costs ~800 cycles on MI355X
+// (tools/microbench.hip), the DPP form a small fraction of that.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace tdstar {
+
+// ---- cross-lane reductions on 64-bit keys through DPP (VALU, no LDS) ----
+// A non-negative double orders like its bit pattern, so distances reduce as
+// unsigned 64-bit keys.  update_dpp returns `old` in lanes whose source is out
+// of the row or masked off, so `old` is the identity of the reduction.
+template <int CTRL, int RM>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v, unsigned long long idn) {
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)idn, (int)(unsigned)v, CTRL, RM, 0xf, false);
+    const int hi =
+        __builtin_amdgcn_update_dpp((int)(unsigned)(idn >> 32), (int)(unsigned)(v >> 32), CTRL, RM, 0xf, false);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+// min over the 64 lanes of the wave, returned to every lane
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+    constexpr unsigned long long I = ~0ull;
+    v = umin64(v, dpp_u64<0x111, 0xf>(v, I));  // row_shr:1
+    v = umin64(v, dpp_u64<0x112, 0xf>(v, I));  // row_shr:2
+    v = umin64(v, dpp_u64<0x114, 0xf>(v, I));  // row_shr:4
+    v = umin64(v, dpp_u64<0x118, 0xf>(v, I));  // row_shr:8  -> lane 15 of a row: row min
+    v = umin64(v, dpp_u64<0x142, 0xa>(v, I));  // row_bcast:15 into rows 1, 3
+    v = umin64(v, dpp_u64<0x143, 0xc>(v, I));  // row_bcast:31 into rows 2, 3 -> lane 63: min
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+// max over each row of 16 lanes, valid in the row's last lane (lane % 16 == 15)
+__device__ __forceinline__ unsigned long long row_max_u64(unsigned long long v) {
+    v = umax64(v, dpp_u64<0x111, 0xf>(v, 0ull));
+    v = umax64(v, dpp_u64<0x112, 0xf>(v, 0ull));
+    v = umax64(v, dpp_u64<0x114, 0xf>(v, 0ull));
+    v = umax64(v, dpp_u64<0x118, 0xf>(v, 0ull));
+    return v;
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+}  // namespace tdstar

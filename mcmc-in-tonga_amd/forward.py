@@ -64,6 +64,13 @@ class TdContext:
         check(lib().td_get_info(self.h, ctypes.byref(info)), self.h)
         self.likelihood_const = float(info.likelihood)
 
+    NN_AUTO, NN_BRUTE, NN_GRID = 0, 1, 2
+
+    def set_nn_method(self, method):
+        """Nearest-cell search: NN_AUTO (bucket grid from 256 cells on), NN_BRUTE
+        (every point x every cell, the reference's loop), NN_GRID.  Same answer."""
+        check(lib().tdt_set_nn_method(self.h, int(method)), self.h)
+
     def timing(self, enable=None, reset=False, kernel=None):
         """Per-kernel HIP-event timing: enable/reset, or read (launches, total_ms) of `kernel`."""
         if enable is not None:

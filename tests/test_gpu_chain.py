@@ -154,3 +154,23 @@ def test_batched_chains_equal_single_launches(tt, ds, ctx):
     for c, (st, m) in zip(batch, solo):
         assert c.stats()["phi"] == st["phi"] and c.stats()["accepted"] == st["accepted"]
         assert same_models(c.model(), m)
+
+
+@pytest.mark.parametrize("ncells,iters,seed", [(300, 300, 61), (2000, 200, 62)])
+def test_hbm_layout_follows_host_engine(tt, ds, ctx, ncells, iters, seed):
+    """The layout larger geometries take (tiles, rays and order in HBM instead
+    of LDS: k_chain_run<false>) against the host engine, bit for bit."""
+    prm = tt.define_TDstructrure().replace(max_cells=ncells + 200)
+    model = tt.random_model(ncells, seed)
+    dev = make(tt, ctx, prm, model, seed, tt.TD_ENGINE_DEVICE)
+    assert tt.lib().tdt_chain_set_lds_mode(dev.h, 1) == 0
+    host = make(tt, ctx, prm, model, seed, tt.TD_ENGINE_HOST)
+    for _ in range(3):
+        dev.run(iters // 3)
+        host.run(iters // 3)
+        assert dev.stats()["phi"] == host.stats()["phi"]
+        assert dev.stats()["accepted"] == host.stats()["accepted"]
+    assert same_models(dev.model(), host.model())
+    m = dev.model()
+    ptS, phi, _, _ = ctx.evaluate(m.cells())
+    assert phi == m.phi and np.array_equal(ptS, m.ptS)

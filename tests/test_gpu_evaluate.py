@@ -188,3 +188,64 @@ def test_stress_full_size_properties(tt):
         d = (dx * dx + dy * dy) + dz * dz
         assert near[q] == int(np.argmin(d))
     c.close()
+
+
+def _both_methods(tt, ctx, orc, ds, cells):
+    out = []
+    for m in (ctx.NN_BRUTE, ctx.NN_GRID):
+        ctx.set_nn_method(m)
+        out.append(ctx.evaluate(cells, want_nearest=True))
+    ctx.set_nn_method(ctx.NN_AUTO)
+    ref = ref_eval(orc, ds, cells)
+    for ptS, phi, _, near in out:
+        assert np.array_equal(near, ref["nearest"])
+        assert np.array_equal(ptS, ref["ptS"]) and phi == ref["phi"]
+
+
+def test_grid_search_adversarial(tt, orc, ds, ctx):
+    """Bucket grid vs brute force vs oracle where a grid is most likely to go
+    wrong: lattice cells (exact ties, points on bucket faces), one tight
+    cluster (every point falls back), planar / collinear cells (degenerate
+    axes), NaN cells, and cells far from every ray."""
+    xmin, xmax, ymin, ymax, zmin, zmax = tt.box()
+    gx, gy, gz = np.meshgrid(np.linspace(xmin, xmax, 12), np.linspace(ymin, ymax, 8), np.linspace(zmin, zmax, 6),
+                             indexing="ij")
+    lat = (gx.ravel(), gy.ravel(), gz.ravel(), np.arange(gx.size, dtype=np.float64) % 47 + 1)
+    _both_methods(tt, ctx, orc, ds, lat)
+    # lattice with integer spacing: ray points land on faces and midpoints often
+    ix, iy, iz = np.meshgrid(np.arange(0, 1000, 50.0), np.arange(-250, 400, 50.0), np.arange(0, 650, 50.0),
+                             indexing="ij")
+    _both_methods(tt, ctx, orc, ds, (ix.ravel(), iy.ravel(), iz.ravel(), np.ones(ix.size) * 3.0 + (ix.ravel() % 7)))
+    rng = np.random.default_rng(4)
+    n = 500
+    clus = (400 + rng.uniform(0, 1, n), 100 + rng.uniform(0, 1, n), 300 + rng.uniform(0, 1, n), rng.uniform(1, 49, n))
+    _both_methods(tt, ctx, orc, ds, clus)
+    planar = (rng.uniform(0, 1000, n), rng.uniform(-250, 400, n), np.full(n, 200.0), rng.uniform(1, 49, n))
+    _both_methods(tt, ctx, orc, ds, planar)
+    line = (rng.uniform(0, 1000, n), np.full(n, 50.0), np.full(n, 100.0), rng.uniform(1, 49, n))
+    _both_methods(tt, ctx, orc, ds, line)
+    m = tt.random_model(600, 8)
+    x, y, z, zeta = (a.copy() for a in m.cells())
+    x[::50] = np.nan
+    z[7::60] = np.nan
+    _both_methods(tt, ctx, orc, ds, (x, y, z, zeta))
+    far = (rng.uniform(5e4, 6e4, n), rng.uniform(5e4, 6e4, n), rng.uniform(0, 10, n), rng.uniform(1, 49, n))
+    _both_methods(tt, ctx, orc, ds, far)
+    mixed = tuple(np.concatenate([a, b]) for a, b in zip(m.cells(), far))
+    _both_methods(tt, ctx, orc, ds, mixed)
+
+
+def test_grid_interpolate_adversarial(tt, orc, ctx):
+    """td_interpolate (grid rasterisation queries) against the oracle with
+    queries on lattice faces, outside the box and NaN-terminated."""
+    rng = np.random.default_rng(12)
+    cells = tt.random_model(2000, 13).cells()
+    X = np.concatenate([np.arange(-100, 1100, 25.0), rng.uniform(-500, 1500, 300), [np.nan, 5.0]])
+    Y = np.concatenate([np.full(48, 50.0), rng.uniform(-500, 800, 300), [0.0, 0.0]])
+    Z = np.concatenate([np.arange(0, 48 * 14, 14.0), rng.uniform(-100, 800, 300), [0.0, 0.0]])
+    for m in (ctx.NN_BRUTE, ctx.NN_GRID):
+        ctx.set_nn_method(m)
+        zr, near = ctx.interpolate(cells, X, Y, Z, want_nearest=True)
+        ref, ref_ids = orc.interpolation(cells, X, Y, Z)
+        assert np.array_equal(zr, ref) and np.array_equal(near, ref_ids)
+    ctx.set_nn_method(ctx.NN_AUTO)
