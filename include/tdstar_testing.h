@@ -43,6 +43,13 @@ int tdt_accept(const td_chain_params *prm, int action, double u_accept, double z
  * in LDS when they fit (the 381-ray configs); 1 keeps them in HBM, the path
  * larger geometries take.  Same results either way. */
 int tdt_chain_set_lds_mode(td_chain *ch, int mode);
+/* The block-wide exact sequential sum (exact_sum.h, used for chi^2 over long
+ * ray lists): prefix[k] = C0 + term[0] + ... + term[k] added strictly left to
+ * right in FP64 (MCsub.jl:170-172).  *fast = 1 when the parallel path proved
+ * its result (else prefix/C_end are untouched and the kernels take the
+ * one-lane loop).  Needs a GPU. */
+int tdt_exact_sum(int device, const double *term, int64_t cnt, double C0, double *prefix, double *C_end, int *fast);
+
 /* Nearest-cell method of td_evaluate / td_interpolate: 0 auto (bucket grid
  * from 256 cells on), 1 brute force (every point x every cell), 2 bucket grid.
  * All give the same answer (the lexicographic (distance, index) minimum). */

@@ -186,7 +186,7 @@ void free_ctx(td_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->timer.release();
-    void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->cells,
+    void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->cells,
                    c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->ptS, c->phi,
                    c->q, c->q_i, c->q_z, c->chain_desc, c->nn.g_count, c->nn.g_ent, c->nn.g_fb};
     for (void *p : dev)
@@ -297,6 +297,7 @@ int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, 
     rc = rc ? rc : dalloc((void **)&c->g.ray_off, sizeof(int) * (size_t)(n + 1), "hipMalloc(ray_off)");
     rc = rc ? rc : dalloc((void **)&c->g.tS, nb, "hipMalloc(tS)");
     rc = rc ? rc : dalloc((void **)&c->g.sig, nb, "hipMalloc(sig)");
+    rc = rc ? rc : dalloc((void **)&c->g.terms, nb, "hipMalloc(terms)");
     rc = rc ? rc : dalloc((void **)&c->best_i, sizeof(int) * (size_t)(P > 0 ? P : 1), "hipMalloc(best_i)");
     rc = rc ? rc : dalloc((void **)&c->best_d, Pb, "hipMalloc(best_d)");
     rc = rc ? rc : dalloc((void **)&c->zeta0, Pb, "hipMalloc(zeta0)");
@@ -461,6 +462,25 @@ int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const 
     std::memcpy(zeta_out, ctx->h_q_z, sizeof(double) * (size_t)np);
     if (nearest_out) std::memcpy(nearest_out, ctx->h_q_i, sizeof(int) * (size_t)np);
     return TD_OK;
+}
+
+int tdt_exact_sum(int device, const double *term, int64_t cnt, double C0, double *prefix, double *C_end,
+                  int *fast) {
+    if (!term || !prefix || !C_end || !fast || cnt < 1 || cnt > (1 << 24)) return TD_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return TD_ERR_HIP;
+    const size_t nb = sizeof(double) * (size_t)cnt;
+    void *buf = nullptr;
+    if (hipMalloc(&buf, 2 * nb + 2 * sizeof(double)) != hipSuccess) return TD_ERR_NOMEM;
+    double *dt = static_cast<double *>(buf), *dp = dt + cnt, *de = dp + cnt;
+    int *df = reinterpret_cast<int *>(de + 1);
+    hipError_t e = hipMemcpy(dt, term, nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = test_exact_sum(dt, (int)cnt, C0, dp, de, df);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(fast, df, sizeof(int), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && *fast) e = hipMemcpy(prefix, dp, nb, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && *fast) e = hipMemcpy(C_end, de, sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(buf);
+    return e == hipSuccess ? TD_OK : TD_ERR_HIP;
 }
 
 int tdt_set_nn_method(td_ctx *ctx, int method) {

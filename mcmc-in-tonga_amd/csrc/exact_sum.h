@@ -1,0 +1,318 @@
+// exact_sum.h -- the sequential sum of MCsub.jl:169-172
+//     C = C0;  for k in 1:n  C += term[k]  end
+// reproduced bit for bit by a whole workgroup, for long sums (the 10k-ray
+// stress geometry: one lane needs ~10k dependent FP64 adds, ~90 us).
+//
+// All terms are >= 0, so the partial sums never decrease.  While C stays in
+// one binade [2^b, 2^(b+1)) every partial sum is M*u with u = 2^(b-52) and
+// 2^52 <= M < 2^53, and one rounded step C + t is an integer step on M:
+//     x = t/u (exact);  f = floor(x);  frac < 1/2: M += f;  > 1/2: M += f+1;
+//     == 1/2: M becomes the even one of M+f, M+f+1   (ties-to-even)
+// i.e. M -> M + D[M mod 2] with two integers D, a class closed under
+// composition.  So a run of terms inside one binade is a SCAN.  The block:
+//   A. sums its chunks and scans the chunk sums (any association) to label
+//      every partial sum with a binade guess; a change of label starts a
+//      segment;
+//   B. turns each term into its step for its label's unit and scans the steps
+//      (segmented: a segment's first term is not a step, see C);
+//   C. thread 0 walks the segments in order: the first term of a segment is
+//      added with an ordinary FP64 add (the reference's own operation), the
+//      rest of the segment is its composed step;
+//   D. checks every guess (each segment's first sum lies in its binade, its
+//      last one below the top) and reports failure otherwise: the caller then
+//      runs the one-lane loop.  The result is always the sequential sum.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+namespace tdstar {
+
+constexpr int kExactMaxSeg = 128;  // binade segments (more: the caller's loop)
+
+struct ExactSumLds {
+    double wsum[16];                  // per-wave totals of the approximate scan
+    unsigned long long wd0[16], wd1[16];
+    int wreset[16], wcnt[16];
+    int first_start[1025];            // does thread j's first term start a segment (+1 sentinel)
+    int last_b[1024];                 // label of thread j's last term
+    int seg_b[kExactMaxSeg];
+    double seg_t[kExactMaxSeg];
+    unsigned long long seg_d0[kExactMaxSeg], seg_d1[kExactMaxSeg], seg_base[kExactMaxSeg];
+    double C_end;
+    int nseg, ok;
+};
+
+namespace exact_detail {
+
+__device__ __forceinline__ int binade(double x) {  // x > 0 normal: floor(log2 x)
+    return (int)(((unsigned long long)__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+}
+__device__ __forceinline__ double pow2(int e) {  // 2^e, -1022 <= e <= 1023
+    return __longlong_as_double((long long)((unsigned long long)(e + 1023) << 52));
+}
+
+// M -> M + d[M & 1]; `reset`: a segment's first term (identity step; scans restart there)
+struct Step {
+    unsigned long long d0, d1;
+    int reset;
+};
+__device__ __forceinline__ Step then(const Step &a, const Step &b) {  // a first, then b
+    if (b.reset) return b;
+    Step r;
+    r.d0 = a.d0 + ((a.d0 & 1ull) ? b.d1 : b.d0);
+    r.d1 = a.d1 + ((a.d1 & 1ull) ? b.d0 : b.d1);
+    r.reset = a.reset;
+    return r;
+}
+// the step of term t in a segment of binade b (not its first term); bad: not representable
+__device__ __forceinline__ Step step_of(double t, int b, bool &bad) {
+    Step e{0ull, 0ull, 0};
+    const double x = t * pow2(52 - b);  // exact: a power-of-two scaling
+    if (!(x < 9007199254740992.0)) {    // >= 2^53 (or NaN): the sum leaves the binade
+        bad = true;
+        return e;
+    }
+    const double f = floor(x);
+    const double r = x - f;  // exact
+    const unsigned long long fi = (unsigned long long)f;
+    if (r < 0.5) {
+        e.d0 = e.d1 = fi;
+    } else if (r > 0.5) {
+        e.d0 = e.d1 = fi + 1ull;
+    } else {                                 // halfway: land on the even integer
+        e.d0 = fi + (fi & 1ull);             // M even: M + f is even iff f is
+        e.d1 = fi + ((fi & 1ull) ^ 1ull);    // M odd:  M + f is even iff f is odd
+    }
+    return e;
+}
+__device__ __forceinline__ unsigned long long apply(const Step &s, unsigned long long M) {
+    return M + ((M & 1ull) ? s.d1 : s.d0);
+}
+
+// exclusive block scans through the wave shuffles + one LDS round (T threads)
+template <int T>
+__device__ double block_excl_f64(double v, ExactSumLds &w) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl = incl + u;
+    }
+    if (lane == 63) w.wsum[wv] = incl;
+    __syncthreads();
+    double base = 0.0;
+    for (int k = 0; k < wv; ++k) base = base + w.wsum[k];
+    __syncthreads();
+    return base + (incl - v);
+}
+template <int T>
+__device__ Step block_excl_step(const Step &v, ExactSumLds &w) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    Step incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        Step u;
+        u.d0 = __shfl_up(incl.d0, o, 64);
+        u.d1 = __shfl_up(incl.d1, o, 64);
+        u.reset = __shfl_up(incl.reset, o, 64);
+        if (lane >= o) incl = then(u, incl);
+    }
+    Step ex;
+    ex.d0 = __shfl_up(incl.d0, 1, 64);
+    ex.d1 = __shfl_up(incl.d1, 1, 64);
+    ex.reset = __shfl_up(incl.reset, 1, 64);
+    if (lane == 0) ex = Step{0ull, 0ull, 0};
+    if (lane == 63) {
+        w.wd0[wv] = incl.d0;
+        w.wd1[wv] = incl.d1;
+        w.wreset[wv] = incl.reset;
+    }
+    __syncthreads();
+    Step base{0ull, 0ull, 0};
+    for (int k = 0; k < wv; ++k) base = then(base, Step{w.wd0[k], w.wd1[k], w.wreset[k]});
+    __syncthreads();
+    return then(base, ex);
+}
+template <int T>
+__device__ int block_excl_int(int v, int &total, ExactSumLds &w) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) w.wcnt[wv] = incl;
+    __syncthreads();
+    int base = 0;
+    total = 0;
+    for (int k = 0; k < T / 64; ++k) {
+        if (k < wv) base += w.wcnt[k];
+        total += w.wcnt[k];
+    }
+    __syncthreads();
+    return base + incl - v;
+}
+
+}  // namespace exact_detail
+
+// The block's T threads (all of them must call) sum term[0..cnt) after C0.
+// On success: *C_end (every thread), prefix[k] = C after term k if prefix is
+// non-null; returns true.  On failure (a guess did not hold) returns false and
+// writes nothing: the caller adds the terms one by one.
+template <int T>
+__device__ bool block_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end,
+                                ExactSumLds &w) {
+    using namespace exact_detail;
+    static_assert(T <= 1024 && T % 64 == 0, "block size");
+    const int tid = threadIdx.x;
+    const int E = (cnt + T - 1) / T;
+    const int lo = min(cnt, tid * E), hi = min(cnt, lo + E);
+    // ---- A: approximate partial sums -> a binade label per term ----
+    double S = 0.0;
+    for (int k = lo; k < hi; ++k) S = S + term[k];
+    const double run0 = C0 + block_excl_f64<T>(S, w);
+    bool bad = !(C0 >= 0.0);
+    {
+        double run = run0;
+        int lb = 0;
+        for (int k = lo; k < hi; ++k) {
+            const double t = term[k];
+            run = run + t;
+            const int b = binade(run);
+            if (!(t >= 0.0) || !(run > 0.0) || !(run < 1e300) || b < -960) bad = true;
+            lb = b;
+        }
+        w.last_b[tid] = lb;
+    }
+    __syncthreads();
+    // ---- B: steps, segment starts, local composition ----
+    auto label_before = [&](int j) { return w.last_b[j]; };
+    Step loc{0ull, 0ull, 0};
+    int nstart = 0;
+    {
+        double run = run0;
+        int pb = 0;
+        // the last label of the nearest earlier thread that owns terms
+        for (int j = tid - 1; j >= 0 && lo > 0; --j) {
+            if (min(cnt, j * E) < min(cnt, j * E + E)) {
+                pb = label_before(j);
+                break;
+            }
+        }
+        for (int k = lo; k < hi; ++k) {
+            const double t = term[k];
+            run = run + t;
+            const int b = binade(run);
+            const bool st = k == 0 || b != pb;
+            Step e{0ull, 0ull, st ? 1 : 0};
+            if (!st) e = step_of(t, b, bad);
+            if (k == lo) w.first_start[tid] = st ? 1 : 0;
+            loc = then(loc, e);
+            nstart += st ? 1 : 0;
+            pb = b;
+        }
+        if (lo >= hi) w.first_start[tid] = 0;
+        if (tid == 0) w.first_start[T] = 1;  // past the end
+    }
+    w.ok = 1;
+    __syncthreads();
+    if (bad) w.ok = 0;
+    int nseg = 0;
+    const int soff = block_excl_int<T>(nstart, nseg, w);  // also a barrier: w.ok is final
+    const Step ex = block_excl_step<T>(loc, w);
+    if (!w.ok || nseg > kExactMaxSeg || nseg < 1) return false;
+    // ---- per segment: binade, first term, composed step of the rest ----
+    {
+        double run = run0;
+        int s = soff - 1, pb = 0;
+        for (int j = tid - 1; j >= 0 && lo > 0; --j)
+            if (min(cnt, j * E) < min(cnt, j * E + E)) {
+                pb = w.last_b[j];
+                break;
+            }
+        Step acc = ex;
+        for (int k = lo; k < hi; ++k) {
+            const double t = term[k];
+            run = run + t;
+            const int b = binade(run);
+            const bool st = k == 0 || b != pb;
+            bool dummy = false;
+            const Step e = st ? Step{0ull, 0ull, 1} : step_of(t, b, dummy);
+            acc = then(acc, e);
+            if (st) {
+                ++s;
+                w.seg_b[s] = b;
+                w.seg_t[s] = t;
+            }
+            // the segment ends here if the next term starts one
+            bool next_st;
+            if (k + 1 < hi) {
+                const double r2 = run + term[k + 1];
+                next_st = binade(r2) != b;
+            } else {
+                int jn = tid + 1;  // the next thread that owns terms
+                while (jn < T && min(cnt, jn * E) >= min(cnt, jn * E + E)) ++jn;
+                next_st = jn >= T || w.first_start[jn] != 0;
+            }
+            if (next_st) {
+                w.seg_d0[s] = acc.d0;
+                w.seg_d1[s] = acc.d1;
+            }
+            pb = b;
+        }
+    }
+    __syncthreads();
+    // ---- C: the segments in order, one thread ----
+    if (tid == 0) {
+        int ok = 1;
+        double C = C0;
+        for (int g = 0; g < nseg && ok; ++g) {
+            if (g > 0) {  // the previous segment's last sum
+                const unsigned long long M0 = w.seg_base[g - 1];
+                const unsigned long long M = M0 + ((M0 & 1ull) ? w.seg_d1[g - 1] : w.seg_d0[g - 1]);
+                if (M >= (1ull << 53)) ok = 0;
+                C = (double)M * pow2(w.seg_b[g - 1] - 52);
+            }
+            C = C + w.seg_t[g];  // the reference's own rounded add
+            if (!(C > 0.0) || binade(C) != w.seg_b[g]) ok = 0;
+            w.seg_base[g] = ok ? (unsigned long long)(C * pow2(52 - w.seg_b[g])) : 0ull;
+        }
+        if (ok) {
+            const unsigned long long M0 = w.seg_base[nseg - 1];
+            const unsigned long long M = M0 + ((M0 & 1ull) ? w.seg_d1[nseg - 1] : w.seg_d0[nseg - 1]);
+            if (M >= (1ull << 53)) ok = 0;
+            w.C_end = (double)M * pow2(w.seg_b[nseg - 1] - 52);
+        }
+        w.ok = ok;
+    }
+    __syncthreads();
+    if (!w.ok) return false;
+    *C_end = w.C_end;
+    // ---- D: every partial sum: its segment's first sum with the step so far ----
+    if (prefix) {
+        double run = run0;
+        int s = soff - 1, pb = 0;
+        for (int j = tid - 1; j >= 0 && lo > 0; --j)
+            if (min(cnt, j * E) < min(cnt, j * E + E)) {
+                pb = w.last_b[j];
+                break;
+            }
+        Step acc = ex;
+        for (int k = lo; k < hi; ++k) {
+            const double t = term[k];
+            run = run + t;
+            const int b = binade(run);
+            const bool st = k == 0 || b != pb;
+            bool dummy = false;
+            const Step e = st ? Step{0ull, 0ull, 1} : step_of(t, b, dummy);
+            acc = then(acc, e);
+            if (st) ++s;
+            prefix[k] = (double)apply(acc, w.seg_base[s]) * pow2(w.seg_b[s] - 52);
+            pb = b;
+        }
+    }
+    return true;
+}
+
+}  // namespace tdstar

@@ -114,6 +114,7 @@ struct Geometry {
     double *px = nullptr, *py = nullptr, *pz = nullptr, *w = nullptr;
     int *ray_off = nullptr;
     double *tS = nullptr, *sig = nullptr;
+    double *terms = nullptr;  // [n] scratch: chi^2 terms of one evaluation
 };
 
 // How a cell set is split over workgroups for the brute-force search.
@@ -141,6 +142,9 @@ hipError_t launch_nearest_grid(const double *qx, const double *qy, const double 
                                int64_t qy_stride, int64_t qz_stride, const double *cells, int64_t stride,
                                int64_t ncells, const CellGrid &G, NNWork &work, int num_cus, int *best_i,
                                double *best_d, double *zeta0, hipStream_t s, Timer *tm = nullptr);
+
+// Testing: the block-wide exact sequential sum (exact_sum.h) on device buffers.
+hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast);
 
 // ptS[i] = julia_sum_j w[j] * ((0.5*(z0[j]+z0[j+1])) / 1000) per ray (MCsub.jl:147-159).
 hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm = nullptr);

@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "internal.h"
+#include "exact_sum.h"
 #include "ray_sum.h"
 
 namespace tdstar {
@@ -129,30 +130,63 @@ __global__ __launch_bounds__(256) void k_ray_sums(const int *__restrict__ ray_of
 }
 
 // ---------------------------------------------------------------------------
-// Stage 3: chi^2, MCsub.jl:169-172.  Terms in parallel into LDS, then one
-// lane adds them in k order (the reference's sequential loop, bit for bit).
+// Stage 3: chi^2, MCsub.jl:169-172, strictly sequential in k.  Terms in
+// parallel, then either one lane adds them in k order (short sums) or the
+// block reproduces that order exactly with binade-segmented integer scans
+// (exact_sum.h; long sums), falling back to the one lane if a guess fails.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_chi2(const double *__restrict__ ptS, const double *__restrict__ tS,
-                                              const double *__restrict__ sig, int n, double *__restrict__ phi) {
-    constexpr int kTile = 2048;
-    __shared__ double t[kTile];
-    double C = 0.0;
-    for (int base = 0; base < n; base += kTile) {
-        const int cnt = min(kTile, n - base);
-        for (int k = threadIdx.x; k < cnt; k += 256) {
-            const double d = ptS[base + k] - tS[base + k];
-            const double s = sig[base + k];
-            t[k] = ((d * d) * 1.0) / (s * s);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0)
-            for (int k = 0; k < cnt; ++k) C = C + t[k];
-        __syncthreads();
+constexpr int kChi2Threads = 1024;
+constexpr int kExactMinTerms = 2048;  // below: the one-lane loop is as fast
+
+__global__ __launch_bounds__(kChi2Threads) void k_chi2(const double *__restrict__ ptS,
+                                                       const double *__restrict__ tS,
+                                                       const double *__restrict__ sig, int n,
+                                                       double *__restrict__ terms, double *__restrict__ phi) {
+    __shared__ ExactSumLds w;
+    for (int k = threadIdx.x; k < n; k += kChi2Threads) {
+        const double d = ptS[k] - tS[k];
+        const double s = sig[k];
+        terms[k] = ((d * d) * 1.0) / (s * s);
     }
-    if (threadIdx.x == 0) *phi = C;
+    __syncthreads();
+    double C = 0.0;
+    bool done = false;
+    if (n >= kExactMinTerms) done = block_exact_sum<kChi2Threads>(terms, n, 0.0, nullptr, &C, w);
+    if (threadIdx.x == 0) {
+        if (!done) {
+            C = 0.0;
+            int k = 0;
+            for (; k + 8 <= n; k += 8) {
+                double t[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) t[u] = terms[k + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) C = C + t[u];
+            }
+            for (; k < n; ++k) C = C + terms[k];
+        }
+        *phi = C;
+    }
+}
+
+__global__ __launch_bounds__(kChi2Threads) void k_test_exact_sum(const double *__restrict__ term, int cnt, double C0,
+                                                                double *__restrict__ prefix, double *C_end,
+                                                                int *fast) {
+    __shared__ ExactSumLds w;
+    double C = 0.0;
+    const bool ok = block_exact_sum<kChi2Threads>(term, cnt, C0, prefix, &C, w);
+    if (threadIdx.x == 0) {
+        *fast = ok ? 1 : 0;
+        if (ok) *C_end = C;
+    }
 }
 
 }  // namespace
+
+hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast) {
+    hipLaunchKernelGGL(k_test_exact_sum, dim3(1), dim3(kChi2Threads), 0, nullptr, term, cnt, C0, prefix, C_end, fast);
+    return hipGetLastError();
+}
 
 NNPlan plan_nearest(int64_t npts, int64_t ncells, int num_cus) {
     NNPlan p{};
@@ -222,7 +256,7 @@ hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, 
 
 hipError_t launch_chi2(const Geometry &g, const double *ptS, double *phi, hipStream_t s, Timer *tm) {
     hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
-    hipLaunchKernelGGL(k_chi2, dim3(1), dim3(256), 0, s, ptS, g.tS, g.sig, (int)g.n, phi);
+    hipLaunchKernelGGL(k_chi2, dim3(1), dim3(kChi2Threads), 0, s, ptS, g.tS, g.sig, (int)g.n, g.terms, phi);
     if (tm) tm->end("chi2", t0, s);
     return hipGetLastError();
 }

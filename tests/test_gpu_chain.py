@@ -174,3 +174,24 @@ def test_hbm_layout_follows_host_engine(tt, ds, ctx, ncells, iters, seed):
     m = dev.model()
     ptS, phi, _, _ = ctx.evaluate(m.cells())
     assert phi == m.phi and np.array_equal(ptS, m.ptS)
+
+
+def test_many_rays_chain_follows_host_engine(tt):
+    """3000 synthetic rays: tiles, rays and order live in HBM and the chi^2
+    tails run through the block-wide exact scan; still bit for bit the host
+    engine (one full evaluate per proposal)."""
+    ds = tt.synthetic_rays(3000, seed=8)
+    ctx = tt.TdContext.from_datastruct(ds)
+    prm = tt.define_TDstructrure().replace(max_cells=900)
+    model = tt.random_model(700, 21)
+    dev = make(tt, ctx, prm, model, 21, tt.TD_ENGINE_DEVICE)
+    host = make(tt, ctx, prm, model, 21, tt.TD_ENGINE_HOST)
+    for _ in range(3):
+        dev.run(40)
+        host.run(40)
+        assert dev.stats()["phi"] == host.stats()["phi"]
+        assert dev.stats()["accepted"] == host.stats()["accepted"]
+    assert same_models(dev.model(), host.model())
+    dev.close()
+    host.close()
+    ctx.close()

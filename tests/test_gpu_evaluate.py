@@ -249,3 +249,18 @@ def test_grid_interpolate_adversarial(tt, orc, ctx):
         ref, ref_ids = orc.interpolation(cells, X, Y, Z)
         assert np.array_equal(zr, ref) and np.array_equal(near, ref_ids)
     ctx.set_nn_method(ctx.NN_AUTO)
+
+
+@pytest.mark.parametrize("ncells", [200, 2500])
+def test_many_rays_exact_chi2(tt, orc, ncells):
+    """10k synthetic rays: chi^2 over 10k terms takes the block-wide exact scan
+    (exact_sum.h) -- phi must still equal the oracle's sequential loop."""
+    ds = tt.synthetic_rays(10000, seed=5)
+    ctx = tt.TdContext.from_datastruct(ds)
+    cells = tt.random_model(ncells, 17).cells()
+    ptS, phi, lk, near = ctx.evaluate(cells, want_nearest=True)
+    ref = ref_eval(orc, ds, cells)
+    assert np.array_equal(near, ref["nearest"])
+    assert np.array_equal(ptS, ref["ptS"])
+    assert phi == ref["phi"] and lk == ref["likelihood"]
+    ctx.close()

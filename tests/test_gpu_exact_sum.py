@@ -1,0 +1,84 @@
+"""GPU: the block-wide exact sequential sum (exact_sum.h) behind chi^2 over
+long ray lists must equal the strictly left-to-right FP64 loop of
+MCsub.jl:170-172 bit for bit whenever it claims success, and claim success
+on realistic data.  Reference: a Python loop of IEEE-754 double adds (the
+same operation sequence as the Julia loop)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def seq(terms, c0):
+    out, c = [], c0
+    for t in terms:
+        c = c + float(t)
+        out.append(c)
+    return np.array(out)
+
+
+def run(tt, terms, c0):
+    terms = np.ascontiguousarray(terms, dtype=np.float64)
+    pre = np.zeros(len(terms))
+    ce = ctypes.c_double()
+    fast = ctypes.c_int()
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    assert tt.lib().tdt_exact_sum(0, P(terms), len(terms), float(c0), P(pre), ctypes.byref(ce),
+                                  ctypes.byref(fast)) == 0
+    return bool(fast.value), pre, ce.value
+
+
+def check(tt, terms, c0):
+    fast, pre, ce = run(tt, terms, c0)
+    if fast:
+        want = seq(terms, c0)
+        bad = np.nonzero(pre != want)[0]
+        assert len(bad) == 0, (bad[:5], pre[bad[:5]], want[bad[:5]])
+        assert ce == want[-1]
+    return fast
+
+
+def test_chi2_like_terms(tt):
+    """(ptS - tS)^2 / sig^2 of a 10k-ray model: the case the kernels meet."""
+    rng = np.random.default_rng(0)
+    hits = 0
+    for trial in range(6):
+        n = [2048, 5000, 10000, 10000, 20000, 3000][trial]
+        d = rng.normal(0, 0.3, n)
+        sig = rng.uniform(0.04, 0.6, n)
+        terms = ((d * d) * 1.0) / (sig * sig)
+        c0 = 0.0 if trial % 2 == 0 else float(seq(rng.exponential(1.0, 50), 0.0)[-1])
+        hits += check(tt, terms, c0)
+    assert hits == 6
+
+
+@pytest.mark.parametrize("cnt", [1, 2, 63, 64, 65, 1023, 1024, 1025, 4097])
+def test_sizes(tt, cnt):
+    rng = np.random.default_rng(cnt)
+    fast = 0
+    for trial in range(4):
+        terms = rng.exponential(rng.choice([1e-3, 1.0, 40.0]), cnt) * rng.choice([1.0, 1e3], cnt)
+        fast += check(tt, terms, 0.0 if trial % 2 == 0 else float(rng.uniform(0, 500)))
+    assert fast >= 3
+
+
+def test_adversarial(tt):
+    # exact halfway terms: ties-to-even decided by the running sum's parity
+    check(tt, np.full(3000, 2.0 ** -53), 1.0)
+    check(tt, np.full(3000, 2.0 ** -53), 1.0 + 2.0 ** -52)
+    check(tt, np.full(3000, 3 * 2.0 ** -53), 1.0)
+    rng = np.random.default_rng(5)
+    half = (rng.integers(1, 9, 4000) * 2 + 1) * 2.0 ** -54  # odd multiples of half an ulp of 1
+    assert check(tt, half, 1.0)
+    # a binade crossing at every term (more segments than the scan keeps)
+    check(tt, 2.0 ** np.arange(300, dtype=np.float64) % 1e300, 1.0)
+    # zeros, a zero start, huge and tiny terms mixed
+    check(tt, np.zeros(2000), 0.0)
+    check(tt, np.concatenate([[0.0, 0.0, 1e-300, 5.0, 0.0, 1e200, 3.0], rng.exponential(1.0, 2000)]), 0.0)
+    check(tt, np.concatenate([[1e-310, 2e-310], rng.exponential(1.0, 2000)]), 0.0)
+    for _ in range(10):
+        check(tt, np.exp(rng.uniform(-40, 40, 3000)), float(rng.uniform(0, 10)))
+    # sums landing exactly on powers of two
+    check(tt, np.concatenate([[0.5, 0.25, 0.25, 1.0, 2.0, 4.0 - 2.0 ** -50, 2.0 ** -50], np.ones(2000)]), 0.0)
