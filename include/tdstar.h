@@ -124,6 +124,22 @@ int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const 
                    int64_t *npoints_out);
 
 /* ------------------------------------------------------------------------
+ * Posterior maps -- the numbers of plot_model_hist (MCsub.jl:753-825), not the
+ * plots.  For nq query points (a cross-section: MCsub.jl:765-768 xz at y =
+ * ySlice, :799-802 xy at z = zSlice) and nmodels saved models (model k's cells
+ * are [cell_off[k], cell_off[k+1]) of the cell arrays, in model_hist order,
+ * chain by chain, MCsub.jl:761-763):
+ *   values_out[k*nq + q] = v_nearest of model k at point q   (nullable)
+ *   mean_out[q] = Statistics.mean over the models            (MCsub.jl:774)
+ *   std_out[q]  = Statistics.std (corrected) over the models (MCsub.jl:775)
+ * with Julia's sum association for a Vector of matrices (raster.hip).
+ * ------------------------------------------------------------------------ */
+int td_rasterize(td_ctx *ctx, int64_t nmodels, const int64_t *cell_off, const double *xCell,
+                 const double *yCell, const double *zCell, const double *zeta, const double *qx,
+                 const double *qy, const double *qz, int64_t nq, double *mean_out, double *std_out,
+                 double *values_out);
+
+/* ------------------------------------------------------------------------
  * rj-MCMC chain -- replaces TD_inversion_function.jl:7-305 (one chain) for
  * prior == 1 (uniform), the default (define_TDstructure.jl:52).  The chain
  * state (cells, per-point nearest-cell cache, ptS, phi) lives in device

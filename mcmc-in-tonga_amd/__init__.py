@@ -19,3 +19,4 @@ from .data import (CONFIGS, ak135_slowness, box, interp1, load_data_Tonga, lonla
 from .defstruct import DataStruct, Model, Ray  # noqa: F401
 from .forward import Interpolation, TdContext, context_for, evaluate, v_nearest  # noqa: F401
 from .tempering import Exchange, TemperingLadder, decide_swaps, geometric_ladder  # noqa: F401
+from .posterior import plot_model_hist, section  # noqa: F401

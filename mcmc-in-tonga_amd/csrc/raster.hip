@@ -1,0 +1,175 @@
+// raster.hip -- posterior maps of plot_model_hist (MCsub.jl:753-825) without
+// the plotting: the nearest-cell value of every saved model at every node of
+// a cross-section (v_nearest, MCsub.jl:765-768 / 799-802), then per node the
+// mean and the standard deviation over the models (MCsub.jl:774-775) in the
+// association Julia's Statistics uses for a Vector of matrices:
+//   mean = sum(A) / n          sum: mapreduce(+) -- n < 16 left to right,
+//                              else pairwise halves down to <= 1024-element
+//                              blocks added left to right (no SIMD
+//                              reassociation: the elements are arrays)
+//   std  = sqrt.(sum(abs2.(A .- mean)) / (n - 1))      (same association)
+// The model sweep reuses the evaluate path's nearest search (bucket grid or
+// brute force per model size), one launch group per model.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "ctx.h"
+
+namespace tdstar {
+
+namespace {
+
+// Julia's mapreduce association over k = 0..n-1 of f(k) (n >= 1).
+template <class F>
+__device__ double julia_mapreduce_seq_blocks(F f, int n) {
+    if (n == 1) return f(0);
+    if (n < 16) {
+        double s = f(0) + f(1);
+        for (int k = 2; k < n; ++k) s = s + f(k);
+        return s;
+    }
+    // pairwise: blocks of <= 1024 elements are summed left to right
+    int lo_s[40], hi_s[40], st_s[40];
+    double vals[40];
+    int top = 1, nv = 0;
+    lo_s[0] = 0;
+    hi_s[0] = n - 1;
+    st_s[0] = 0;
+    while (top > 0) {
+        const int lo = lo_s[top - 1], hi = hi_s[top - 1];
+        if (hi - lo < 1024) {
+            double s = f(lo) + f(lo + 1);
+            for (int k = lo + 2; k <= hi; ++k) s = s + f(k);
+            vals[nv++] = s;
+            --top;
+            continue;
+        }
+        const int mid = (lo + hi) >> 1;
+        if (st_s[top - 1] == 0) {
+            st_s[top - 1] = 1;
+            lo_s[top] = lo; hi_s[top] = mid; st_s[top] = 0; ++top;
+        } else if (st_s[top - 1] == 1) {
+            st_s[top - 1] = 2;
+            lo_s[top] = mid + 1; hi_s[top] = hi; st_s[top] = 0; ++top;
+        } else {
+            const double v2 = vals[--nv];
+            const double v1 = vals[--nv];
+            vals[nv++] = v1 + v2;
+            --top;
+        }
+    }
+    return vals[0];
+}
+
+__global__ __launch_bounds__(256) void k_raster_stats(const double *__restrict__ values, int nmodels, int nq,
+                                                      double *__restrict__ mean, double *__restrict__ sd) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const double *v = values + q;
+    const long st = nq;
+    const double m = julia_mapreduce_seq_blocks([&](int k) { return v[k * st]; }, nmodels) / (double)nmodels;
+    const double ss = julia_mapreduce_seq_blocks(
+        [&](int k) {
+            const double d = v[k * st] - m;
+            return d * d;  // abs2
+        },
+        nmodels);
+    mean[q] = m;
+    sd[q] = sqrt(ss / (double)(nmodels - 1));  // corrected; n == 1 gives 0/0 = NaN as in Julia
+}
+
+}  // namespace
+
+}  // namespace tdstar
+
+using namespace tdstar;
+
+extern "C" int td_rasterize(td_ctx *ctx, int64_t nmodels, const int64_t *cell_off, const double *xCell,
+                            const double *yCell, const double *zCell, const double *zeta, const double *qx,
+                            const double *qy, const double *qz, int64_t nq, double *mean_out, double *std_out,
+                            double *values_out) {
+    if (!ctx) return set_err(nullptr, TD_ERR_ARG, "td_rasterize: ctx is NULL");
+    if (nmodels < 1 || !cell_off || nq < 0 || (nq > 0 && (!qx || !qy || !qz || !mean_out || !std_out)))
+        return set_err(ctx, TD_ERR_ARG, "td_rasterize: bad arguments");
+    const int64_t total = cell_off[nmodels];
+    if (cell_off[0] != 0 || total < 0 || (total > 0 && (!xCell || !yCell || !zCell || !zeta)))
+        return set_err(ctx, TD_ERR_ARG, "td_rasterize: bad cell offsets or arrays");
+    for (int64_t k = 0; k < nmodels; ++k)
+        if (cell_off[k + 1] < cell_off[k]) return set_err(ctx, TD_ERR_ARG, "td_rasterize: offsets not monotone");
+    if (nq == 0) return TD_OK;
+    if (nq > 0x7fffffff / std::max<int64_t>(nmodels, 1) || total > 0x7fffffff)
+        return set_err(ctx, TD_ERR_ARG, "td_rasterize: too large");
+    TD_HIP(ctx, hipSetDevice(ctx->device));
+    // one device block: queries (3 nq), all cells SoA (4 total), values (nmodels nq), mean, std (2 nq)
+    const size_t nd = 3 * (size_t)nq + 4 * (size_t)std::max<int64_t>(total, 1) + (size_t)nmodels * nq + 2 * (size_t)nq;
+    if (nd > ctx->raster_cap) {
+        if (ctx->raster) (void)hipFree(ctx->raster);
+        ctx->raster = nullptr;
+        ctx->raster_cap = 0;
+        TD_HIP(ctx, hipMalloc(&ctx->raster, sizeof(double) * nd));
+        ctx->raster_cap = nd;
+    }
+    double *dq = ctx->raster, *dc = dq + 3 * nq, *dv = dc + 4 * std::max<int64_t>(total, 1), *dm = dv + nmodels * nq,
+           *ds = dm + nq;
+    const int64_t cs = std::max<int64_t>(total, 1);  // SoA stride of the cells
+    std::vector<double> h(3 * (size_t)nq + 4 * (size_t)cs);
+    std::memcpy(h.data(), qx, sizeof(double) * (size_t)nq);
+    std::memcpy(h.data() + nq, qy, sizeof(double) * (size_t)nq);
+    std::memcpy(h.data() + 2 * nq, qz, sizeof(double) * (size_t)nq);
+    double *hc = h.data() + 3 * nq;
+    if (total > 0) {
+        std::memcpy(hc, xCell, sizeof(double) * (size_t)total);
+        std::memcpy(hc + cs, yCell, sizeof(double) * (size_t)total);
+        std::memcpy(hc + 2 * cs, zCell, sizeof(double) * (size_t)total);
+        std::memcpy(hc + 3 * cs, zeta, sizeof(double) * (size_t)total);
+    }
+    if (nq > ctx->raster_i_cap) {  // nearest-cell indices (not returned)
+        if (ctx->raster_i) (void)hipFree(ctx->raster_i);
+        ctx->raster_i = nullptr;
+        ctx->raster_i_cap = 0;
+        TD_HIP(ctx, hipMalloc(&ctx->raster_i, sizeof(int) * (size_t)nq));
+        ctx->raster_i_cap = nq;
+    }
+    TD_HIP(ctx, hipMemcpyAsync(dq, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, ctx->stream));
+    Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
+    for (int64_t k = 0; k < nmodels; ++k) {
+        const int64_t a = cell_off[k], nc = cell_off[k + 1] - a;
+        double *out = dv + k * nq;
+        hipError_t e;
+        if (nc >= kGridMinCells && ctx->nn_method != 1) {
+            double lo[3], hi[3];
+            const double *src[3] = {xCell + a, yCell + a, zCell + a};
+            for (int d = 0; d < 3; ++d) {
+                double l = HUGE_VAL, u = -HUGE_VAL;
+                for (int64_t i = 0; i < nc; ++i) {
+                    l = src[d][i] < l ? src[d][i] : l;
+                    u = src[d][i] > u ? src[d][i] : u;
+                }
+                lo[d] = l <= u ? l : 0.0;
+                hi[d] = l <= u ? u : 0.0;
+            }
+            const CellGrid G = make_cell_grid(lo, hi, (double)nc / 2.0, 4096, kGridMaxBuckets);
+            e = launch_nearest_grid(dq, dq + nq, dq + 2 * nq, nq, 1, 1, dc + a, cs, nc, G, ctx->nn, ctx->num_cus,
+                                    ctx->raster_i, nullptr, out, ctx->stream, tm);
+        } else {
+            e = launch_nearest(dq, dq + nq, dq + 2 * nq, nq, 1, 1, dc + a, cs, nc, ctx->nn, ctx->num_cus,
+                               ctx->raster_i, nullptr, out, ctx->stream, tm);
+        }
+        if (e != hipSuccess) return hip_err(ctx, e, "td_rasterize: nearest kernels");
+    }
+    hipLaunchKernelGGL(k_raster_stats, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ctx->stream, dv,
+                       (int)nmodels, (int)nq, dm, ds);
+    TD_HIP(ctx, hipGetLastError());
+    TD_HIP(ctx, hipMemcpyAsync(mean_out, dm, sizeof(double) * (size_t)nq, hipMemcpyDeviceToHost, ctx->stream));
+    TD_HIP(ctx, hipMemcpyAsync(std_out, ds, sizeof(double) * (size_t)nq, hipMemcpyDeviceToHost, ctx->stream));
+    if (values_out)
+        TD_HIP(ctx, hipMemcpyAsync(values_out, dv, sizeof(double) * (size_t)nq * nmodels, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    TD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return TD_OK;
+}

@@ -108,6 +108,20 @@ class TdContext:
                                       ptr(phi), ptr(lk)), self.h)
         return ptS, phi, lk
 
+    def rasterize(self, models, qx, qy, qz, want_values=False):
+        """td_rasterize: -> (mean[nq], std[nq], values[nmodels, nq] or None).
+        models: list of (x, y, z, zeta) cell arrays in model_hist order."""
+        off = np.zeros(len(models) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(m[0]) for m in models])
+        cat = [f64(np.concatenate([np.asarray(m[k], dtype=np.float64) for m in models])) for k in range(4)]
+        qx, qy, qz = (f64(np.ravel(a)) for a in (qx, qy, qz))
+        nq = len(qx)
+        mean, std = np.empty(nq), np.empty(nq)
+        vals = np.empty((len(models), nq)) if want_values else None
+        check(lib().td_rasterize(self.h, len(models), ptr(off, _lib._pi64), *(ptr(c) for c in cat), ptr(qx), ptr(qy),
+                                 ptr(qz), nq, ptr(mean), ptr(std), ptr(vals) if want_values else None), self.h)
+        return mean, std, vals
+
     def interpolate(self, cells, X, Y, Z, want_nearest=False):
         """-> (zeta[npoints], nearest[npoints] or None)"""
         xc, yc, zc, ze = (f64(c) for c in cells)

@@ -107,3 +107,47 @@ def evaluate_csr(npts, px, py, pz, w, tS, allSig, cells):
         ptS[i] = julia_sum(terms)
         off += c
     return ptS, chi2(ptS, tS, allSig), likelihood(allSig), idx
+
+
+def julia_mapreduce_arrays(vals):
+    """sum over a Vector of arrays (Base.mapreduce for non-bitstype elements):
+    n < 16 left to right; else pairwise halves (mid = (lo+hi)>>1) down to
+    blocks of <= 1024 elements, each added left to right (the @simd loop cannot
+    reassociate array additions).  vals: list of float64 arrays (same shape)."""
+    n = len(vals)
+    if n == 1:
+        return vals[0].copy()
+    if n < 16:
+        s = vals[0] + vals[1]
+        for v in vals[2:]:
+            s = s + v
+        return s
+
+    def impl(lo, hi):
+        if hi - lo < 1024:
+            s = vals[lo] + vals[lo + 1]
+            for k in range(lo + 2, hi + 1):
+                s = s + vals[k]
+            return s
+        mid = (lo + hi) >> 1
+        return impl(lo, mid) + impl(mid + 1, hi)
+
+    return impl(0, n - 1)
+
+
+def rasterize(models, qx, qy, qz):
+    """plot_model_hist (MCsub.jl:761-775): the v_nearest value of every model at
+    every query point, then Statistics.mean and std (corrected) over the models
+    -- mean = sum(A)/n, std = sqrt.(sum(abs2.(A .- mean)) / (n-1)), both sums
+    in the association above.  models: list of (x, y, z, zeta) arrays."""
+    vals = []
+    for xc, yc, zc, ze in models:
+        idx = nearest_index(qx, qy, qz, xc, yc, zc)
+        ze = np.asarray(ze, dtype=np.float64)
+        vals.append(np.where(idx >= 0, ze[np.maximum(idx, 0)] if len(ze) else 0.0, 0.0))
+    n = len(vals)
+    mean = julia_mapreduce_arrays(vals) / float(n)
+    dev = [(v - mean) * (v - mean) for v in vals]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        std = np.sqrt(julia_mapreduce_arrays(dev) / float(n - 1))
+    return mean, std, np.array(vals)
