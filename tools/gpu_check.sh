@@ -1,3 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -m pytest tests/test_gpu_posterior.py -x -q > gpurun_out/t_post.log 2>&1 || { echo "posterior tests failed"; exit 1; }
+timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1 || { echo "bench failed"; exit 1; }
+bash tools/profile.sh r01_v6 || { echo "profile failed"; exit 1; }
