@@ -113,14 +113,17 @@ __device__ __forceinline__ void make_proposal(PState &o, const tdchain::Params &
 }
 
 struct Shared {
-    PState cur, spec;  // this iteration's proposal; the next one, guessed during phase F
-    int spec_ok;
+    PState ps[2];      // this iteration's proposal (ps[cur]) and the next one guessed in phase F
+    int cur, spec_ok;
     double phi_n;
     int accept;
     int n_tiles, n_changed, n_orphans, n_rays, k0;
     int pts_seen, ray_pts;
     // bucket-grid update of an accepted proposal (applied by the last wave in phase G)
     int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site
+    // what the update needs from the grid, read during phase F (G only writes)
+    int gp_bo, gp_co, gp_pos, gp_bn, gp_cn;
+    BucketEntry gp_last;
     double g_ox, g_oy, g_oz, g_nx, g_ny, g_nz;
     // chain scalars, resident for the whole launch
     long long iter, evaluations, bytes;
@@ -340,27 +343,54 @@ __device__ __forceinline__ Nearest wave_nearest(const DevChain &d, const Views &
     return r;
 }
 
-// Apply the pending bucket-grid update (one wave).
-__device__ void grid_apply(const DevChain &d, Shared &sh, int lane) {
+// Read what the bucket-grid update of an accepted proposal will need (one
+// wave, during phase F, before the decision): the old site's bucket, count,
+// the slot's position in it and its last entry; the new site's bucket and count.
+__device__ void grid_prefetch(const DevChain &d, Shared &sh, int lane, int action, int slot, double ox, double oy,
+                              double oz, double nx, double ny, double nz) {
+    const bool rm = action == tdchain::kDeath || action == tdchain::kMove;
+    const bool ins = action == tdchain::kBirth || action == tdchain::kMove;
+    int bo = 0, co = 0, pos = -1, bn = 0, cn = 0;
+    if (rm) {
+        bo = grid_bucket(d.grid, ox, oy, oz);
+        co = d.bucket_count[bo];
+        const int s = lane < kBucketCap ? d.buckets[bo * kBucketCap + lane].slot : -1;
+        const unsigned long long m = __ballot(lane < co && s == slot);
+        pos = m ? __builtin_ctzll(m) : -1;
+        if (lane == 0 && co > 0) sh.gp_last = d.buckets[bo * kBucketCap + co - 1];
+    }
+    if (ins) {
+        bn = grid_bucket(d.grid, nx, ny, nz);
+        cn = d.bucket_count[bn];
+    }
+    if (lane == 0) {
+        sh.gp_bo = bo;
+        sh.gp_co = co;
+        sh.gp_pos = pos;
+        sh.gp_bn = bn;
+        sh.gp_cn = cn;
+    }
+}
+
+// Apply the accepted proposal's bucket-grid update from the prefetched data
+// (lane 0 of one wave; stores only).
+__device__ void grid_apply(const DevChain &d, Shared &sh) {
     const int op = sh.g_op;
-    if (op & 1) {  // remove g_slot from the bucket of its old site
-        const int b = grid_bucket(d.grid, sh.g_ox, sh.g_oy, sh.g_oz);
-        const int cnt = d.bucket_count[b];
-        const int s = lane < kBucketCap ? d.buckets[b * kBucketCap + lane].slot : -1;
-        const unsigned long long m = __ballot(lane < cnt && s == sh.g_slot);
-        if (lane == 0) {
-            if (m == 0ull) {
-                *d.grid_overflow = 1;  // bookkeeping lost track: stop trusting the grid
-                sh.grid_ovf = 1;
-            } else {
-                d.buckets[b * kBucketCap + __builtin_ctzll(m)] = d.buckets[b * kBucketCap + cnt - 1];
-                d.bucket_count[b] = cnt - 1;
-            }
+    int co = sh.gp_co;
+    if (op & 1) {  // remove g_slot: the bucket's last entry takes its place
+        const int b = sh.gp_bo, pos = sh.gp_pos;
+        if (pos < 0) {
+            *d.grid_overflow = 1;  // bookkeeping lost track: stop trusting the grid
+            sh.grid_ovf = 1;
+        } else {
+            d.buckets[b * kBucketCap + pos] = sh.gp_last;
+            d.bucket_count[b] = co - 1;
+            co -= 1;
         }
     }
-    if ((op & 2) && lane == 0) {  // insert at the new site
-        const int b = grid_bucket(d.grid, sh.g_nx, sh.g_ny, sh.g_nz);
-        const int cnt = d.bucket_count[b];
+    if (op & 2) {  // insert at the new site
+        const int b = sh.gp_bn;
+        const int cnt = ((op & 1) && b == sh.gp_bo) ? co : sh.gp_cn;  // a move inside one bucket
         if (cnt < kBucketCap) {
             d.buckets[b * kBucketCap + cnt] = BucketEntry{sh.g_nx, sh.g_ny, sh.g_nz, sh.g_slot, 0};
             d.bucket_count[b] = cnt + 1;
@@ -488,6 +518,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.iter = s0.iter;
         sh.evaluations = 0;
         sh.bytes = 0;
+        sh.cur = 0;
         sh.grid_fallbacks32 = 0;
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
@@ -507,9 +538,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
         wave_sync_lds();
         if (lane == 0 && iters > 0) {
-            make_proposal(sh.cur, P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
+            make_proposal(sh.ps[0], P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
                           d.czeta, [&](int pos) { return v.ord[pos]; });
-            if (sh.cur.p.active) sh.proposed[sh.cur.p.action] += 1;
+            if (sh.ps[0].p.active) sh.proposed[sh.ps[0].p.action] += 1;
             sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
             sh.pts_seen = sh.ray_pts = 0;
             sh.k0 = n;
@@ -521,12 +552,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
 
     for (long long it = 0; it < iters; ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
-        const Proposal p = sh.cur.p;
+        const PState &cur = sh.ps[sh.cur];
+        const Proposal p = cur.p;
         const int action = p.action;
         const int ncells = sh.ncells;
-        const int slot_k = sh.cur.slot_k;
-        const bool eval = sh.cur.eval != 0;
-        const double kx = sh.cur.kx, ky = sh.cur.ky, kz = sh.cur.kz;
+        const int slot_k = cur.slot_k;
+        const bool eval = cur.eval != 0;
+        const double kx = cur.kx, ky = cur.ky, kz = cur.kz;
+        const int new_slot = cur.new_slot;
+        const double zeta_killed = cur.zeta_killed;
         double czeta = 0.0, zetanew_death = 0.0;
         STAMP(0);
         if (p.active) {
@@ -540,11 +574,19 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 const TileQuery tq0 = tile_query(kx, ky, kz), tq1 = tile_query(p.x, p.y, p.z);
                 const int nthr = query ? kChainThreads - 64 : kChainThreads;
                 if (tid < nthr)
-                    for (int t = tid; t < NT; t += nthr) {
-                        const float thr = tile_thr(v.tmaxd[t]);
-                        const bool hit = (q0 && tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr)) ||
-                                         (q1 && tile_may_hit(v.tlo, v.thi, NT, t, tq1, thr));
-                        if (hit) v.thit[atomicAdd(&sh.n_tiles, 1)] = t;
+                    for (int t0 = tid; t0 < NT; t0 += 3 * nthr) {  // three tiles in flight per thread
+                        bool hit[3];
+#pragma unroll
+                        for (int u = 0; u < 3; ++u) {
+                            const int t = min(t0 + u * nthr, NT - 1);  // clamped: loads stay unconditional
+                            const float thr = tile_thr(v.tmaxd[t]);
+                            const bool h0 = tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr);
+                            const bool h1 = tile_may_hit(v.tlo, v.thi, NT, t, tq1, thr);
+                            hit[u] = t0 + u * nthr < NT && ((q0 && h0) || (q1 && h1));
+                        }
+#pragma unroll
+                        for (int u = 0; u < 3; ++u)
+                            if (hit[u]) v.thit[atomicAdd(&sh.n_tiles, 1)] = t0 + u * nthr;
                     }
             }
             if (action == tdchain::kDeath)  // deleteat! shift, staged before we know if it is accepted
@@ -585,7 +627,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     const double qx = d.px[q], qy = d.py[q], qz = d.pz[q];
                     if (action == tdchain::kBirth) {  // appended cell: strict capture
                         const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
-                        if (dd < bd) mark(d, v, sh, q, ray, sh.cur.new_slot, dd, pp.zeta);
+                        if (dd < bd) mark(d, v, sh, q, ray, new_slot, dd, pp.zeta);
                     } else if (action == tdchain::kChange) {
                         if (s == slot_k) mark(d, v, sh, q, ray, s, bd, pp.zeta);
                     } else if (s == slot_k) {  // death / move: its points are re-searched
@@ -694,7 +736,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                                 (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28;
                 }
                 // Metropolis-Hastings decision
-                const bool acc = tdchain::accept(P, pp, ncells, sh.phi, phi_n, czeta, sh.cur.zeta_killed,
+                const bool acc = tdchain::accept(P, pp, ncells, sh.phi, phi_n, czeta, zeta_killed,
                                                  zetanew_death);
                 sh.accept = acc ? 1 : 0;
                 sh.phi_n = phi_n;
@@ -702,7 +744,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.accepted[action] += 1;
                     sh.g_op = action == tdchain::kBirth ? 2 : action == tdchain::kDeath ? 1
                               : action == tdchain::kMove ? 3 : 0;
-                    sh.g_slot = action == tdchain::kBirth ? sh.cur.new_slot : slot_k;
+                    sh.g_slot = action == tdchain::kBirth ? new_slot : slot_k;
                     sh.g_ox = kx;
                     sh.g_oy = ky;
                     sh.g_oz = kz;
@@ -712,14 +754,18 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 }
             } else if (tid == 64) {  // the next proposal as if this one were rejected
                 if (can_spec) {
-                    make_proposal(sh.spec, P, draws[(it + 1) & 63], ncells, sh.nfree, sh.nslots, d.free_slots, d.cx,
+                    make_proposal(sh.ps[sh.cur ^ 1], P, draws[(it + 1) & 63], ncells, sh.nfree, sh.nslots, d.free_slots, d.cx,
                                   d.cy, d.cz, d.czeta, [&](int pos) { return v.ord[pos]; });
                     sh.spec_ok = 1;
                 }
+            } else if (wv == kWaves - 1) {  // the grid data an accepted update will need
+                if (action != tdchain::kChange)
+                    grid_prefetch(d, sh, lane, action, action == tdchain::kBirth ? new_slot : slot_k, kx, ky,
+                                  kz, pp.x, pp.y, pp.z);
             } else if (wv >= 2 && fwd && action != tdchain::kChange) {
                 // the hit tiles' maxima if the proposal is accepted (a tile = a DPP row)
                 const int nt = sh.n_tiles;
-                for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 128) {
+                for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 192) {
                     const int t = v.thit[i / kTilePts];
                     const int q = v.tstart[t] + (i % kTilePts);
                     unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
@@ -758,11 +804,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         v.ord[j - 1] = s;
                         d.rank[s] = j - 1;
                     }
-                if (wv == kWaves - 1 && sh.g_op) grid_apply(d, sh, lane);
+                if (tid == kChainThreads - 64 && sh.g_op) grid_apply(d, sh);
                 if (tid == 0) {
                     const int sk = slot_k;
                     if (action == tdchain::kBirth) {  // append!
-                        const int s = sh.cur.new_slot;
+                        const int s = new_slot;
                         d.cx[s] = pp.x;
                         d.cy[s] = pp.y;
                         d.cz[s] = pp.z;
@@ -797,6 +843,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 }
             }
         }
+        STAMP(12);
         // ===== end of iteration: the next proposal (wave 0; draws refilled every 64) =====
         if (wv == 0) {
             if (lane == 0) {
@@ -814,18 +861,18 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     // the guess holds unless an accepted proposal changed what it read
                     const bool keep = sh.spec_ok && can_spec &&
                                       (!acc || ((action == tdchain::kChange || action == tdchain::kMove) &&
-                                                sh.spec.slot_k != slot_k));
+                                                sh.ps[sh.cur ^ 1].slot_k != slot_k));
                     if (keep) {
-                        sh.cur = sh.spec;
+                        sh.cur ^= 1;  // adopt the guess: no copy
                     } else {
                         // a just-killed position: later positions read the pre-shift order
                         const int killed = (acc && action == tdchain::kDeath) ? (int)pp.index : -1;
-                        make_proposal(sh.cur, P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots, d.free_slots,
+                        make_proposal(sh.ps[sh.cur], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots, d.free_slots,
                                       d.cx, d.cy, d.cz, d.czeta, [&](int pos) {
                                           return (killed >= 0 && pos >= killed) ? d.order_tmp[pos + 1] : v.ord[pos];
                                       });
                     }
-                    if (sh.cur.p.active) sh.proposed[sh.cur.p.action] += 1;
+                    if (sh.ps[sh.cur].p.active) sh.proposed[sh.ps[sh.cur].p.action] += 1;
                     sh.spec_ok = 0;
                     sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
                     sh.pts_seen = sh.ray_pts = 0;
@@ -834,6 +881,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 }
             }
         }
+        STAMP(13);
         __syncthreads();
         STAMP(6);
     }

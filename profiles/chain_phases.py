@@ -40,6 +40,7 @@ def main():
     out = (ctypes.c_int64 * 16)()
     L.tdt_chain_profile(ch.h, 0, out)
     cyc = np.array(out[:7], dtype=np.float64) - np.array(out0[:7], dtype=np.float64)
+    cyc[6] += (out[12] - out0[12]) + (out[13] - out0[13])  # G = commit + next proposal + barrier
     fallbacks = int(out[15] - out0[15])
     tot = cyc.sum()
     st1 = ch.stats()
@@ -50,7 +51,11 @@ def main():
            "cycles_per_iter": tot / iters, "grid_fallbacks": fallbacks,
            "phases": {p: {"share": round(c / tot, 4), "cycles_per_iter": round(c / iters, 1)}
                       for p, c in zip(PHASES, cyc)},
-           "cycles_per_proposal_by_action": per_action}
+           "cycles_per_proposal_by_action": per_action,
+           "G sub-phases per iter (tid 0)": {
+               "commit": round((out[12] - out0[12]) / iters, 1),
+               "next proposal": round((out[13] - out0[13]) / iters, 1),
+               "final barrier": round((out[6] - out0[6]) / iters, 1)}}
     print(json.dumps(res, indent=1))
 
 
