@@ -138,7 +138,9 @@ int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z,
     int rc = ensure_cells(ctx, ncells);
     if (rc) return rc;
     if (ncells == 0) return TD_OK;
-    const int64_t s = ctx->cell_cap;
+    // packed SoA with stride ncells: one copy over PCIe
+    const int64_t s = ncells;
+    ctx->cell_stride = s;
     double *h = ctx->h_cells;
     std::memcpy(h, x, sizeof(double) * (size_t)ncells);
     std::memcpy(h + s, y, sizeof(double) * (size_t)ncells);
@@ -155,10 +157,8 @@ int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z,
         ctx->cell_lo[a] = lo <= hi ? lo : 0.0;
         ctx->cell_hi[a] = lo <= hi ? hi : 0.0;
     }
-    // four slices of the SoA (one copy if the set fills the capacity)
-    for (int k = 0; k < 4; ++k)
-        TD_HIP(ctx, hipMemcpyAsync(ctx->cells + k * s, h + k * s, sizeof(double) * (size_t)ncells,
-                                   hipMemcpyHostToDevice, ctx->stream));
+    TD_HIP(ctx, hipMemcpyAsync(ctx->cells, h, sizeof(double) * 4 * (size_t)ncells, hipMemcpyHostToDevice,
+                               ctx->stream));
     return TD_OK;
 }
 
@@ -169,10 +169,10 @@ hipError_t nearest_uploaded(td_ctx *ctx, const double *qx, const double *qy, con
     const bool grid = ctx->nn_method == 2 || (ctx->nn_method == 0 && ncells >= kGridMinCells);
     if (grid && ncells > 0) {
         const CellGrid G = make_cell_grid(ctx->cell_lo, ctx->cell_hi, (double)ncells / 2.0, 4096, kGridMaxBuckets);
-        return launch_nearest_grid(qx, qy, qz, npts, qy_stride, qz_stride, ctx->cells, ctx->cell_cap, ncells, G,
+        return launch_nearest_grid(qx, qy, qz, npts, qy_stride, qz_stride, ctx->cells, ctx->cell_stride, ncells, G,
                                    ctx->nn, ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm);
     }
-    return launch_nearest(qx, qy, qz, npts, qy_stride, qz_stride, ctx->cells, ctx->cell_cap, ncells, ctx->nn,
+    return launch_nearest(qx, qy, qz, npts, qy_stride, qz_stride, ctx->cells, ctx->cell_stride, ncells, ctx->nn,
                           ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm);
 }
 
@@ -187,7 +187,7 @@ void free_ctx(td_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->timer.release();
     void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->cells,
-                   c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->ptS, c->phi,
+                   c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->phi,
                    c->q, c->q_i, c->q_z, c->chain_desc, c->nn.g_count, c->nn.g_ent, c->nn.g_fb, c->raster, c->raster_i};
     for (void *p : dev)
         if (p) (void)hipFree(p);
@@ -301,8 +301,9 @@ int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, 
     rc = rc ? rc : dalloc((void **)&c->best_i, sizeof(int) * (size_t)(P > 0 ? P : 1), "hipMalloc(best_i)");
     rc = rc ? rc : dalloc((void **)&c->best_d, Pb, "hipMalloc(best_d)");
     rc = rc ? rc : dalloc((void **)&c->zeta0, Pb, "hipMalloc(zeta0)");
-    rc = rc ? rc : dalloc((void **)&c->ptS, nb, "hipMalloc(ptS)");
-    rc = rc ? rc : dalloc((void **)&c->phi, sizeof(double), "hipMalloc(phi)");
+    // [phi, ptS[n]] adjacent: one copy back per evaluate
+    rc = rc ? rc : dalloc((void **)&c->phi, sizeof(double) * (size_t)(n + 1), "hipMalloc(phi, ptS)");
+    if (!rc) c->ptS = c->phi + 1;
     if (rc) return fail(rc);
     e = hipHostMalloc(&c->h_out, sizeof(double) * (size_t)(n + 1), hipHostMallocDefault);
     if (e != hipSuccess) return fail(hip_err(c, e, "hipHostMalloc(out)"));
@@ -379,10 +380,8 @@ int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const dou
     if (e != hipSuccess) return hip_err(ctx, e, "ray-sum kernel");
     e = launch_chi2(g, ctx->ptS, ctx->phi, ctx->stream, tm);
     if (e != hipSuccess) return hip_err(ctx, e, "chi2 kernel");
-    TD_HIP(ctx, hipMemcpyAsync(ctx->h_out, ctx->phi, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    if (g.n)
-        TD_HIP(ctx, hipMemcpyAsync(ctx->h_out + 1, ctx->ptS, sizeof(double) * (size_t)g.n, hipMemcpyDeviceToHost,
-                                   ctx->stream));
+    TD_HIP(ctx, hipMemcpyAsync(ctx->h_out, ctx->phi, sizeof(double) * (size_t)(g.n + 1), hipMemcpyDeviceToHost,
+                               ctx->stream));
     if (nearest_out && g.P)
         TD_HIP(ctx, hipMemcpyAsync(ctx->h_best_i, ctx->best_i, sizeof(int) * (size_t)g.P, hipMemcpyDeviceToHost,
                                    ctx->stream));

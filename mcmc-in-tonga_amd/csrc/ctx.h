@@ -20,8 +20,9 @@ struct td_ctx {
     std::vector<double> sig_host;
     double likelihood = 0.0;            // MCsub.jl:179 constant for sig_host
 
-    // one cell set (SoA x|y|z|zeta with stride cell_cap), device + pinned host staging
+    // one cell set (SoA x|y|z|zeta, stride cell_stride <= cell_cap), device + pinned host staging
     double *cells = nullptr;
+    int64_t cell_stride = 1;            // SoA stride of the uploaded cells (= their count)
     double *h_cells = nullptr;
     int64_t cell_cap = 0;
 
