@@ -89,8 +89,16 @@ def main():
         import torch
         import torch.distributed as dist
 
+        # rehearsal knobs (one GPU box): TD_BENCH_BACKEND=gloo TD_BENCH_DEVICE=0 runs every rank on
+        # device 0 with CPU collectives; the driver's runs use RCCL, one rank per GPU
+        backend = os.environ.get("TD_BENCH_BACKEND", "nccl")
+        local = int(os.environ.get("TD_BENCH_DEVICE", local))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    coll_dev = "cuda" if os.environ.get("TD_BENCH_BACKEND", "nccl") == "nccl" else "cpu"
 
     import tonga
 
@@ -105,7 +113,7 @@ def main():
               for j in range(C)]
     ladder = None
     if a.swap_every > 0:
-        ex = tt.Exchange(dist, "cuda") if dist is not None else tt.Exchange()
+        ex = tt.Exchange(dist, coll_dev) if dist is not None else tt.Exchange()
         ladder = tt.TemperingLadder(chains, ex, tmax=a.tmax, seed=4242)
 
     def run_step(k):
@@ -150,7 +158,7 @@ def main():
     if dist is not None:
         import torch
 
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     iters = a.steps * a.iters_per_step
