@@ -64,12 +64,45 @@ __global__ __launch_bounds__(kNNThreads) void k_nn_partial(
     }
     __syncthreads();
 
-#pragma unroll 2
-    for (int j = 0; j < nc; ++j) {
+    // groups of kGroup cells: the group minimum takes one v_min per distance
+    // (instead of compare + three selects); only when it beats the running
+    // best is the first cell reaching it looked up -- rare after the first
+    // groups.  Exactly MCsub.jl:255's strict '<' in index order: the minimum
+    // is one of the distances, a tie inside the group goes to its first cell,
+    // a tie with an earlier group keeps the earlier cell.
+    constexpr int kGroup = 8;
+    int j = 0;
+    for (; j + kGroup <= nc; j += kGroup) {
+        double dg[PPL][kGroup];
+        double m[PPL];
+#pragma unroll
+        for (int u = 0; u < kGroup; ++u) {
+            const double4 c = sc[j + u];
+#pragma unroll
+            for (int k = 0; k < PPL; ++k) {
+                // (mx[i]-x)^2 + (my[i]-y)^2 + (mz[i]-z)^2, MCsub.jl:254, left to right, unfused
+                const double dx = c.x - x[k], dy = c.y - y[k], dz = c.z - z[k];
+                double d = dx * dx;
+                d = d + dy * dy;
+                d = d + dz * dz;
+                dg[k][u] = d;
+                m[k] = u == 0 ? d : fmin(m[k], d);  // fmin: a NaN distance never becomes the minimum
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PPL; ++k)
+            if (m[k] < bd[k]) {  // strict: NaN never wins
+                int f = kGroup - 1;
+#pragma unroll
+                for (int u = kGroup - 1; u >= 0; --u) f = dg[k][u] == m[k] ? u : f;
+                bd[k] = m[k];
+                bi[k] = c0 + j + f;
+            }
+    }
+    for (; j < nc; ++j) {  // the tail, one cell at a time
         const double4 c = sc[j];
 #pragma unroll
         for (int k = 0; k < PPL; ++k) {
-            // (mx[i]-x)^2 + (my[i]-y)^2 + (mz[i]-z)^2, MCsub.jl:254, left to right, unfused
             const double dx = c.x - x[k], dy = c.y - y[k], dz = c.z - z[k];
             double d = dx * dx;
             d = d + dy * dy;
