@@ -223,7 +223,7 @@ hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix
 
 NNPlan plan_nearest(int64_t npts, int64_t ncells, int num_cus) {
     NNPlan p{};
-    p.ppl = 2;
+    p.ppl = npts >= 65536 ? 4 : 2;  // more points per lane once there are blocks enough for every CU
     const int64_t per_block = (int64_t)kNNThreads * p.ppl;
     p.blocks_x = (int)std::max<int64_t>(1, (npts + per_block - 1) / per_block);
     if (ncells <= 0) {
@@ -264,9 +264,14 @@ hipError_t launch_nearest(const double *qx, const double *qy, const double *qz, 
         dim3 grid(p.blocks_x, p.chunks);
         const size_t lds = (size_t)p.chunk * sizeof(double4);
         hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
-        hipLaunchKernelGGL(k_nn_partial<2>, grid, dim3(kNNThreads), lds, s, qx, qy, qz, (int)npts,
-                           (int)qy_stride, (int)qz_stride, cells, (int)stride, (int)ncells, p.chunk,
-                           work.part_d, work.part_i);
+        if (p.ppl == 4)
+            hipLaunchKernelGGL(k_nn_partial<4>, grid, dim3(kNNThreads), lds, s, qx, qy, qz, (int)npts,
+                               (int)qy_stride, (int)qz_stride, cells, (int)stride, (int)ncells, p.chunk,
+                               work.part_d, work.part_i);
+        else
+            hipLaunchKernelGGL(k_nn_partial<2>, grid, dim3(kNNThreads), lds, s, qx, qy, qz, (int)npts,
+                               (int)qy_stride, (int)qz_stride, cells, (int)stride, (int)ncells, p.chunk,
+                               work.part_d, work.part_i);
         if (tm) tm->end("nn_partial", t0, s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
