@@ -64,6 +64,9 @@ tdchain::Params make_params(const td_chain_params &p) {
     P.yr = ((double)p.sig / 100.0) * (p.ymax - p.ymin);
     P.zr = ((double)p.sig / 100.0) * (p.zmax - p.zmin);
     P.temperature = p.temperature > 0.0 ? p.temperature : 1.0;
+    const double two_pi_sqrt = 2.5066282746310002;
+    P.log_prior_birth = std::log((P.sig_zeta * two_pi_sqrt) / P.zeta_scale);
+    P.log_prior_death = std::log(P.zeta_scale / (P.sig_zeta * two_pi_sqrt));
     return P;
 }
 
@@ -146,7 +149,9 @@ int host_iteration(td_chain *ch) {
         rc = host_interp1(ch, nx, ny, nz, nzeta, ch->x[k], ch->y[k], ch->z[k], &zetanew);
         if (rc) return rc;
     }
-    if (tdchain::accept(P, p, N, ch->phi, phi_n, czeta, zeta_killed, zetanew)) {
+    double lnN[3];
+    tdchain::log_window(lnN, N);
+    if (tdchain::accept(P, p, ch->phi, phi_n, czeta, zeta_killed, zetanew, lnN)) {
         ch->x.swap(nx); ch->y.swap(ny); ch->z.swap(nz); ch->zeta.swap(nzeta);
         ch->phi = phi_n;
         ch->ptS.swap(ptS_n);
@@ -220,7 +225,7 @@ int device_setup(td_chain *ch) {
     const size_t Pn = (size_t)std::max<int64_t>(P, 1), nn = (size_t)std::max<int64_t>(n, 1);
     add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * Pn);
     add(sizeof(float) * 3 * ntiles); add(sizeof(float) * 3 * ntiles); add(sizeof(double) * (ntiles + 1)); add(sizeof(double) * (ntiles + 1));
-    add(sizeof(double) * 4 * cap); for (int i = 0; i < 4; ++i) add(sizeof(int) * cap);
+    add(sizeof(double) * 4 * cap); add(sizeof(double) * (cap + 2)); for (int i = 0; i < 4; ++i) add(sizeof(int) * cap);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn); add(Pn);
     add(sizeof(int) * Pn); add(sizeof(int) * Pn); add(sizeof(int) * (ntiles + 1));
@@ -249,6 +254,8 @@ int device_setup(td_chain *ch) {
     d.ntiles = ntiles;
     double *cells = carve<double>(cur, 4 * (size_t)cap);
     d.cx = cells; d.cy = cells + cap; d.cz = cells + 2 * cap; d.czeta = cells + 3 * cap;
+    double *logN_d = carve<double>(cur, (size_t)cap + 2);
+    d.logN = logN_d;
     d.order = carve<int>(cur, cap); d.rank = carve<int>(cur, cap);
     d.free_slots = carve<int>(cur, cap); d.order_tmp = carve<int>(cur, cap);
     d.cap = cap;
@@ -289,7 +296,10 @@ int device_setup(td_chain *ch) {
     s0.nslots = N;
     s0.nfree = 0;
     s0.phi = 1.0;  // debug_prior: evaluate returns phi = 1 (MCsub.jl:131)
+    std::vector<double> logN((size_t)cap + 2);  // logN[k] = det_log(k): the MH model-size factor
+    for (size_t k = 0; k < logN.size(); ++k) logN[k] = tdchain::det_log((double)k);
     struct Up { void *d; const void *h; size_t b; } ups[] = {
+        {logN_d, logN.data(), sizeof(double) * logN.size()},
         {tile_start, tstart.data(), sizeof(int) * tstart.size()},
         {tile_ray_d, tray.data(), sizeof(int) * tray.size()},
         {pt_ray_d, pt_ray.data(), sizeof(int) * (size_t)P},
@@ -592,7 +602,10 @@ int tdt_accept(const td_chain_params *prm, int action, double u_accept, double z
     p.valid = 1;
     p.u_accept = u_accept;
     p.zeta = zeta_new;
-    return tdchain::accept(P, p, ncells, phi, phi_n, czeta, zeta_killed, zetanew_death) ? 1 : 0;
+    p.log_u = u_accept > 0.0 ? tdchain::det_log(u_accept) : -HUGE_VAL;
+    double lnN[3];
+    tdchain::log_window(lnN, ncells);
+    return tdchain::accept(P, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -57,6 +57,7 @@ struct DevChain {
     int ntiles;
     // cells by slot
     double *cx, *cy, *cz, *czeta;  // [cap]
+    const double *logN;            // [cap+2] det_log(k), the MH model-size factor
     int *order, *rank, *free_slots, *order_tmp;  // [cap]
     int cap;
     // per-point cache (current state) and candidate overlay

@@ -115,6 +115,7 @@ __device__ __forceinline__ void make_proposal(PState &o, const tdchain::Params &
 struct Shared {
     PState ps[2];      // this iteration's proposal (ps[cur]) and the next one guessed in phase F
     int cur, spec_ok;
+    int early_reject;  // phase F: the decision is "reject" whatever the remaining chi^2 terms
     double phi_n;
     int accept;
     int n_tiles, n_changed, n_orphans, n_rays, k0;
@@ -130,6 +131,7 @@ struct Shared {
     long long proposed[5], accepted[5];
     double phi;
     int ncells, nslots, nfree;
+    double lnN[3];  // logN[ncells - 1 .. ncells + 1]
     double q_zeta;         // result of the birth/death Interpolation query
     int grid_fallbacks32;  // grid searches that needed the full scan
     int grid_ovf;          // LDS copy of *d.grid_overflow
@@ -519,10 +521,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.evaluations = 0;
         sh.bytes = 0;
         sh.cur = 0;
+        sh.early_reject = 0;
         sh.grid_fallbacks32 = 0;
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
         sh.ncells = s0.ncells;
+        for (int k = 0; k < 3; ++k) sh.lnN[k] = d.logN[max(s0.ncells - 1 + k, 0)];
         sh.nslots = s0.nslots;
         sh.nfree = s0.nfree;
         sh.g_op = 0;
@@ -710,6 +714,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     double C = big ? C_big : (k0 > 0 ? v.prefix[k0 - 1] : 0.0);  // MCsub.jl:169 C = 0
                     int k = big ? n : k0;
                     for (; k + 8 <= n; k += 8) {
+                        // the last wave may prove meanwhile that no remaining sum can be accepted
+                        if (__hip_atomic_load(&sh.early_reject, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                         double t[8], c[8];
 #pragma unroll
                         for (int u = 0; u < 8; ++u) t[u] = v.term[k + u];
@@ -721,10 +727,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
 #pragma unroll
                         for (int u = 0; u < 8; ++u) v.cprefix[k + u] = c[u];
                     }
-                    for (; k < n; ++k) {
-                        C = C + v.term[k];
-                        v.cprefix[k] = C;
-                    }
+                    if (k + 8 > n)
+                        for (; k < n; ++k) {
+                            C = C + v.term[k];
+                            v.cprefix[k] = C;
+                        }
                     phi_n = k0 < n ? C : sh.phi;
                     sh.evaluations += 1;
                     // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
@@ -735,9 +742,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                                 (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
                                 (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28;
                 }
-                // Metropolis-Hastings decision
-                const bool acc = tdchain::accept(P, pp, ncells, sh.phi, phi_n, czeta, zeta_killed,
-                                                 zetanew_death);
+                // Metropolis-Hastings decision (a proven rejection skips the rest of the sum:
+                // accept() on the exact phi_n would reject too)
+                const bool early = fwd && k0 < n && sh.early_reject;
+                if (prof_on && early) sh.prof[14] += 1;  // diagnostic: proven rejections
+                const bool acc = !early && tdchain::accept(P, pp, sh.phi, phi_n, czeta, zeta_killed,
+                                                           zetanew_death, sh.lnN);
                 sh.accept = acc ? 1 : 0;
                 sh.phi_n = phi_n;
                 if (acc) {
@@ -762,10 +772,28 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 if (action != tdchain::kChange)
                     grid_prefetch(d, sh, lane, action, action == tdchain::kBirth ? new_slot : slot_k, kx, ky,
                                   kz, pp.x, pp.y, pp.z);
+            } else if (wv == kWaves - 2) {
+                // a lower bound of phi_n from all new terms: the sequential sum of n
+                // non-negative terms is within n ulps of any other association; above
+                // the rejection bound by a wide margin, the proposal is rejected
+                const int k0 = sh.k0;
+                if (fwd && k0 < n) {
+                    double part = 0.0;
+                    for (int k = k0 + lane; k < n; k += 64) part = part + v.term[k];
+                    const double S = wave_sum_f64(part);
+                    if (lane == 0) {
+                        const double C0 = k0 > 0 ? v.prefix[k0 - 1] : 0.0;
+                        const double lb = (C0 + S) * (1.0 - 1e-9);
+                        const double thr =
+                            tdchain::reject_bound(P, pp, sh.phi, czeta, zeta_killed, zetanew_death, sh.lnN);
+                        if (lb > thr + 1e-7 * (fabs(thr) + fabs(sh.phi)) + 1e-6)
+                            __hip_atomic_store(&sh.early_reject, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
             } else if (wv >= 2 && fwd && action != tdchain::kChange) {
                 // the hit tiles' maxima if the proposal is accepted (a tile = a DPP row)
                 const int nt = sh.n_tiles;
-                for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 192) {
+                for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 256) {
                     const int t = v.thit[i / kTilePts];
                     const int q = v.tstart[t] + (i % kTilePts);
                     unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
@@ -820,11 +848,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         else
                             sh.nslots += 1;
                         sh.ncells = ncells + 1;
+                        for (int k = 0; k < 3; ++k) sh.lnN[k] = d.logN[ncells + k];
                     } else if (action == tdchain::kDeath) {
                         d.free_slots[sh.nfree] = sk;
                         sh.nfree += 1;
                         d.rank[sk] = -1;
                         sh.ncells = ncells - 1;
+                        for (int k = 0; k < 3; ++k) sh.lnN[k] = d.logN[ncells - 2 + k];
                     } else if (action == tdchain::kChange) {
                         d.czeta[sk] = pp.zeta;
                     } else {
@@ -874,6 +904,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     }
                     if (sh.ps[sh.cur].p.active) sh.proposed[sh.ps[sh.cur].p.action] += 1;
                     sh.spec_ok = 0;
+                    sh.early_reject = 0;
                     sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
                     sh.pts_seen = sh.ray_pts = 0;
                     sh.k0 = n;

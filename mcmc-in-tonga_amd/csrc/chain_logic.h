@@ -60,9 +60,11 @@ enum Slot : uint32_t { kSlotAction = 0, kSlotXY = 1, kSlotZZeta = 2, kSlotIndex 
 struct Draws {
     double u_action, u_accept, u_a, u_b, u_c, u_zeta, u_index;
     double z_a, z_b, z_c, z_zeta;  // standard-normal quantiles of u_a, u_b, u_c, u_zeta
+    double log_u;                  // log(u_accept): only for the early-rejection bound (reject_bound)
 };
 
 TD_HD double normal_quantile(double p);
+TD_HD double det_log(double x);
 
 TD_HD Draws draw_iteration(uint64_t seed, uint32_t chain, uint64_t iter) {
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -85,6 +87,7 @@ TD_HD Draws draw_iteration(uint64_t seed, uint32_t chain, uint64_t iter) {
     r.z_b = normal_quantile(r.u_b);
     r.z_c = normal_quantile(r.u_c);
     r.z_zeta = normal_quantile(r.u_zeta);
+    r.log_u = r.u_accept > 0.0 ? det_log(r.u_accept) : -__builtin_huge_val();
     return r;
 }
 
@@ -211,6 +214,9 @@ struct Params {
     double xmin, xmax, ymin, ymax, zmin, zmax;
     double xr, yr, zr;                     // (sig/100)*(max-min), :30-32
     double temperature;
+    // log of the constant prior factors of the birth / death ratios (:96-97,
+    // :151-152), for reject_bound only (host libm; the bound has a wide margin)
+    double log_prior_birth, log_prior_death;
 };
 
 // What the iteration proposes, before any forward-model evaluation.
@@ -223,6 +229,7 @@ struct Proposal {
     double zeta;      // change: new value (birth: filled after czeta is known)
     double z_zeta;    // birth: standard normal for zetanew ~ Normal(czeta, sig_zeta)
     double u_accept;
+    double log_u;     // log(u_accept), for reject_bound
 };
 
 // TD_inversion_function.jl:72 (action = rand(1:4)) and the draws of each
@@ -232,6 +239,7 @@ TD_HD Proposal propose(const Params &P, const Draws &d, int64_t ncells) {
     p.action = 1 + (int)(d.u_action * 4.0);
     if (p.action > 4) p.action = 4;
     p.u_accept = d.u_accept;
+    p.log_u = d.log_u;
     p.z_zeta = d.z_zeta;
     p.valid = 1;
     p.active = 1;
@@ -281,35 +289,53 @@ TD_HD void birth_zeta(const Params &P, Proposal &p, double czeta) {
     p.valid = (p.zeta > 0.0 && p.zeta < P.zeta_scale) ? 1 : 0;
 }
 
-// log of the acceptance ratio (before min(1, .)), prior == 1 (uniform).
+// {log(N-1), log(N), log(N+1)} for log_alpha (the device engine reads the same
+// det_log values from a table built on the host)
+inline void log_window(double out[3], int64_t N) {
+    for (int k = 0; k < 3; ++k) out[k] = det_log((double)(N - 1 + k));
+}
+
+// The Metropolis-Hastings decision, prior == 1 (uniform): rand < min(1, alpha)
+// with alpha of eqs. 14-17 (TD_inversion_function.jl:96-97 birth, :151-152
+// death, :196 change, :241 move), decided in the log domain:
+//     log u < log alpha = log f + g + (phi - phi_n)/(2T)
+// (u < 1, so the min(1, .) never matters; the same decision as comparing u
+// with alpha, without an exp on the critical path).  lnN = {log(N-1), log N,
+// log(N+1)} (det_log), so the model-size factor is lnN[1] - lnN[1 +- 1].
 // extra: birth -> czeta, death -> zetanew = Interpolation(modeln, killed site) (:146)
-TD_HD bool accept(const Params &P, const Proposal &p, int64_t ncells, double phi, double phi_n, double czeta,
-                  double zeta_killed, double zetanew_death) {
-    if (!p.active || !p.valid) return false;
-    const double dphi = (phi_n - phi) / (2.0 * P.temperature);
-    const double two_pi_sqrt = 2.5066282746310002;  // sqrt(2*pi)
-    double alpha;
-    switch (p.action) {
-        case kBirth: {  // eq. 16, :96-97
-            const double N = (double)ncells;
-            const double dz = czeta - p.zeta;
-            alpha = (N / (N + 1.0)) * ((P.sig_zeta * two_pi_sqrt) / P.zeta_scale) *
-                    det_exp((dz * dz) / (2.0 * P.sig_zeta * P.sig_zeta) - dphi);
-            break;
-        }
-        case kDeath: {  // eq. 17, :151-152
-            const double N = (double)ncells;
-            const double dz = zeta_killed - zetanew_death;
-            alpha = (N / (N - 1.0)) * (P.zeta_scale / (P.sig_zeta * two_pi_sqrt)) *
-                    det_exp(-(dz * dz) / (2.0 * P.sig_zeta * P.sig_zeta) - dphi);
-            break;
-        }
-        default:  // change eq. 15 (:196), move eq. 14 (:241)
-            alpha = det_exp(-dphi);
-            break;
+// Written as one if-chain into one variable: a `switch` with a `return -x`
+// default was miscompiled for gfx950 (the default path returned a stale
+// register; tools/repro_accept.hip).
+TD_HD double log_alpha(const Params &P, const Proposal &p, double phi, double phi_n, double czeta,
+                       double zeta_killed, double zetanew_death, const double *lnN) {
+    const double g = (phi - phi_n) / (2.0 * P.temperature);  // change eq. 15 (:196), move eq. 14 (:241)
+    double la = g;
+    if (p.action == kBirth) {  // eq. 16, :96-97: (N/(N+1)) (sig_zeta sqrt(2 pi) / zeta_scale) exp(dz^2/(2 sig^2) - dphi)
+        const double dz = czeta - p.zeta;
+        la = ((lnN[1] - lnN[2]) + P.log_prior_birth) + ((dz * dz) / (2.0 * P.sig_zeta * P.sig_zeta) + g);
+    } else if (p.action == kDeath) {  // eq. 17, :151-152: (N/(N-1)) (zeta_scale / (sig_zeta sqrt(2 pi))) exp(-dz^2/(2 sig^2) - dphi)
+        const double dz = zeta_killed - zetanew_death;
+        la = ((lnN[1] - lnN[0]) + P.log_prior_death) + (g - (dz * dz) / (2.0 * P.sig_zeta * P.sig_zeta));
     }
-    if (alpha > 1.0) alpha = 1.0;  // min([1 alpha]...)
-    return p.u_accept < alpha;    // rand(1)[1] < alpha && valid == 1
+    return la;
+}
+TD_HD bool accept(const Params &P, const Proposal &p, double phi, double phi_n, double czeta, double zeta_killed,
+                  double zetanew_death, const double *lnN) {
+    if (!p.active || !p.valid) return false;  // rand(1)[1] < alpha && valid == 1
+    return p.log_u < log_alpha(P, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN);
+}
+
+// The phi_n from which accept() rejects: log_alpha is dphi-affine, so
+//     reject  <=>  phi_n >= phi + 2T (log f + g - log u)
+// (f, g as in log_alpha).  For deciding before phi_n is known exactly (the
+// chi^2 partial sums only grow); the caller adds a margin far above every
+// rounding involved, so the outcome is the one accept() gives on the exact
+// phi_n.  +inf when no finite bound exists (u == 0).
+TD_HD double reject_bound(const Params &P, const Proposal &p, double phi, double czeta, double zeta_killed,
+                          double zetanew_death, const double *lnN) {
+    if (!(p.u_accept > 0.0)) return __builtin_huge_val();
+    const double lf = log_alpha(P, p, phi, phi, czeta, zeta_killed, zetanew_death, lnN);  // dphi = 0
+    return phi + 2.0 * P.temperature * (lf - p.log_u);
 }
 
 }  // namespace tdchain

@@ -48,4 +48,17 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// sum over the 64 lanes (any association: for bounds, not for results), to every lane
+__device__ __forceinline__ double wave_sum_f64(double v) {
+    auto add = [](double a, unsigned long long b) { return a + __longlong_as_double((long long)b); };
+    auto bits = [](double a) { return (unsigned long long)__double_as_longlong(a); };
+    v = add(v, dpp_u64<0x111, 0xf>(bits(v), 0ull));  // row_shr: inclusive scan inside rows
+    v = add(v, dpp_u64<0x112, 0xf>(bits(v), 0ull));
+    v = add(v, dpp_u64<0x114, 0xf>(bits(v), 0ull));
+    v = add(v, dpp_u64<0x118, 0xf>(bits(v), 0ull));
+    v = add(v, dpp_u64<0x142, 0xa>(bits(v), 0ull));  // row_bcast:15
+    v = add(v, dpp_u64<0x143, 0xc>(bits(v), 0ull));  // row_bcast:31 -> lane 63: the total
+    return readlane_f64(v, 63);
+}
+
 }  // namespace tdstar

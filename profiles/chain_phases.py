@@ -52,6 +52,8 @@ def main():
            "phases": {p: {"share": round(c / tot, 4), "cycles_per_iter": round(c / iters, 1)}
                       for p, c in zip(PHASES, cyc)},
            "cycles_per_proposal_by_action": per_action,
+           "early_rejections": int(out[14] - out0[14]),
+           "rejections": int(sum(prop) - (sum(ch.stats()["accepted"]) - sum(st0["accepted"]))),
            "G sub-phases per iter (tid 0)": {
                "commit": round((out[12] - out0[12]) / iters, 1),
                "next proposal": round((out[13] - out0[13]) / iters, 1),
