@@ -32,9 +32,11 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
  * read the accumulated shader cycles: [0..6] phases A..G of k_chain_run
  * (draw, tiles + birth/death query, points, orphans, ray sums, chi^2 +
  * accept, commit), [8..11] whole proposals by action (birth, death, change,
- * move), [15] grid searches that fell back to a full scan.  Never enabled in
- * measured runs. */
-int tdt_chain_profile(td_chain *ch, int enable, int64_t out[16]);
+ * move), [12..13] commit / next proposal, [14] proven early rejections, [15]
+ * grid searches that fell back to a full scan, [16 + 10 (action-1) + j] the
+ * phases split by action (j: A..F, commit, next proposal, final barrier).
+ * Never enabled in measured runs. */
+int tdt_chain_profile(td_chain *ch, int enable, int64_t out[64]);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);
@@ -49,6 +51,11 @@ int tdt_chain_set_lds_mode(td_chain *ch, int mode);
  * its result (else prefix/C_end are untouched and the kernels take the
  * one-lane loop).  Needs a GPU. */
 int tdt_exact_sum(int device, const double *term, int64_t cnt, double C0, double *prefix, double *C_end, int *fast);
+/* The one-wave exact sequential sum (exact_sum.h wave_seq_sum, the chain's
+ * chi^2 tail): same contract as tdt_exact_sum, always exact; *fallbacks =
+ * 256-term chunks that needed the slower binade-by-binade path.  Needs a GPU. */
+int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, double *prefix, double *C_end,
+                     int *fallbacks);
 
 /* Nearest-cell method of td_evaluate / td_interpolate: 0 auto (bucket grid
  * from 256 cells on), 1 brute force (every point x every cell), 2 bucket grid.

@@ -482,6 +482,25 @@ int tdt_exact_sum(int device, const double *term, int64_t cnt, double C0, double
     return e == hipSuccess ? TD_OK : TD_ERR_HIP;
 }
 
+int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, double *prefix, double *C_end,
+                     int *fallbacks) {
+    if (!term || !prefix || !C_end || !fallbacks || cnt < 1 || cnt > (1 << 24)) return TD_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return TD_ERR_HIP;
+    const size_t nb = sizeof(double) * (size_t)cnt;
+    void *buf = nullptr;
+    if (hipMalloc(&buf, 2 * nb + 2 * sizeof(double)) != hipSuccess) return TD_ERR_NOMEM;
+    double *dt = static_cast<double *>(buf), *dp = dt + cnt, *de = dp + cnt;
+    int *df = reinterpret_cast<int *>(de + 1);
+    hipError_t e = hipMemcpy(dt, term, nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = test_wave_seq_sum(dt, (int)cnt, C0, dp, de, df);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(prefix, dp, nb, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(C_end, de, sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(fallbacks, df, sizeof(int), hipMemcpyDeviceToHost);
+    (void)hipFree(buf);
+    return e == hipSuccess ? TD_OK : TD_ERR_HIP;
+}
+
 int tdt_set_nn_method(td_ctx *ctx, int method) {
     if (!ctx || method < 0 || method > 2) return TD_ERR_ARG;
     ctx->nn_method = method;

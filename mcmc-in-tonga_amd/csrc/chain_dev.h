@@ -26,6 +26,7 @@
 namespace tdstar {
 
 constexpr int kTilePts = 16;
+constexpr int kProfSlots = 64;
 constexpr int kChainThreads = 512;  // 8 waves: 256 VGPRs per lane, no spills
 constexpr int kBucketCap = 32;
 
@@ -36,7 +37,8 @@ struct ChainScalars {
     int64_t proposed[5];
     double phi;
     int64_t bytes;         // algorithmic global-memory bytes the proposals needed (roofline)
-    int64_t prof[16];      // diagnostic: shader cycles per phase (DevChain::profile); [15] grid fallbacks
+    int64_t prof[kProfSlots];  // diagnostic (DevChain::profile): cycles per phase [0..13], [14] proven
+                               // rejections, [15] grid fallbacks, [16 + 10 (action-1) + j] per-action phases
     int ncells;            // cells in the model
     int nslots;            // slot high-water mark
     int nfree;             // free-slot stack depth

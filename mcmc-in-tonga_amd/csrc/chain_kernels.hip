@@ -136,7 +136,7 @@ struct Shared {
     int grid_fallbacks32;  // grid searches that needed the full scan
     int grid_ovf;          // LDS copy of *d.grid_overflow
     OrphanRec orph[kOrphanLds];
-    long long prof[16], t_last, t_iter;  // diagnostic phase stamps
+    long long prof[kProfSlots], t_last, t_iter;  // diagnostic phase stamps
 };
 
 // Diagnostic phase stamp (lane 0 of wave 0, right after a barrier): cycles
@@ -146,6 +146,8 @@ struct Shared {
         if (prof_on && tid == 0) {                 \
             const long long t_ = clock64();        \
             sh.prof[k] += t_ - sh.t_last;          \
+            sh.prof[16 + 10 * (action - 1) +       \
+                    ((k) <= 5 ? (k) : (k) == 12 ? 6 : (k) == 13 ? 7 : 8)] += t_ - sh.t_last; \
             sh.t_last = t_;                        \
         }                                          \
     } while (0)
@@ -531,7 +533,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.nfree = s0.nfree;
         sh.g_op = 0;
         sh.grid_ovf = *d.grid_overflow;
-        for (int k = 0; k < 16; ++k) sh.prof[k] = 0;
+        for (int k = 0; k < kProfSlots; ++k) sh.prof[k] = 0;
         sh.t_last = clock64();
     }
     __syncthreads();
@@ -705,34 +707,26 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                                                          *reinterpret_cast<ExactSumLds *>(lds + L.exact));
                 }
             }
-            if (tid == 0) {
-                double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
+            const long long tF = prof_on ? clock64() : 0;  // diagnostic: per-wave time in F
+            double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
+            if (wv == 0) {
                 const int k0 = sh.k0;
                 if (fwd) {
-                    // ONE lane adds the terms in k order (MCsub.jl:170-172); phase E put
-                    // the changed rays' new terms in place (the old ones wait in cterm)
+                    // the terms added in k order (MCsub.jl:170-172), bit for bit, by this
+                    // wave (exact_sum.h); phase E put the changed rays' new terms in place
+                    // (the old ones wait in cterm).  The last wave may prove meanwhile that
+                    // no remaining sum can be accepted (sh.early_reject): the sum stops.
                     double C = big ? C_big : (k0 > 0 ? v.prefix[k0 - 1] : 0.0);  // MCsub.jl:169 C = 0
-                    int k = big ? n : k0;
-                    for (; k + 8 <= n; k += 8) {
-                        // the last wave may prove meanwhile that no remaining sum can be accepted
-                        if (__hip_atomic_load(&sh.early_reject, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-                        double t[8], c[8];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) t[u] = v.term[k + u];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) {
-                            C = C + t[u];
-                            c[u] = C;
-                        }
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) v.cprefix[k + u] = c[u];
+                    if (!big && k0 < n) {
+                        bool stopped = false;
+                        C = wave_seq_sum(v.term + k0, n - k0, C, v.cprefix + k0, lane, &sh.early_reject, &stopped);
                     }
-                    if (k + 8 > n)
-                        for (; k < n; ++k) {
-                            C = C + v.term[k];
-                            v.cprefix[k] = C;
-                        }
                     phi_n = k0 < n ? C : sh.phi;
+                }
+            }
+            if (tid == 0) {
+                const int k0 = sh.k0;
+                if (fwd) {
                     sh.evaluations += 1;
                     // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
                     // candidate points (coords + cached slot/distance, 36 B), grid queries
@@ -805,6 +799,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     if ((i % kTilePts) == kTilePts - 1) v.ctm[i / kTilePts] = __longlong_as_double((long long)mk);
                 }
             }
+            if (prof_on && lane == 0)
+                atomicAdd((unsigned long long *)&sh.prof[56 + wv], (unsigned long long)(clock64() - tF));
             __syncthreads();
             STAMP(5);
             // ================= phase G: commit (or undo) =================
@@ -939,7 +935,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         s.ncells = sh.ncells;
         s.nslots = sh.nslots;
         s.nfree = sh.nfree;
-        for (int k = 0; k < 15; ++k) s.prof[k] += sh.prof[k];
+        for (int k = 0; k < kProfSlots; ++k) s.prof[k] += sh.prof[k];
         s.prof[15] += sh.grid_fallbacks32;  // diagnostic: unproven grid searches
     }
 }

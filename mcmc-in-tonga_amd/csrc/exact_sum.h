@@ -27,6 +27,8 @@
 #include <climits>
 #include <cstdint>
 
+#include "wave_ops.h"
+
 namespace tdstar {
 
 constexpr int kExactMaxSeg = 128;  // binade segments (more: the caller's loop)
@@ -313,6 +315,82 @@ __device__ bool block_exact_sum(const double *term, int cnt, double C0, double *
         }
     }
     return true;
+}
+
+// ---- one wave: the sequential sum of a short tail (the chain's chi^2) ----
+// out[k] = C_k with C_k = C_{k-1} + t[k] (C_{-1} = C), k = 0..cnt-1, FP64 left
+// to right -- the loop of MCsub.jl:170-172 bit for bit; returns C_{cnt-1}.
+// The binade argument above without its general tie handling: while C stays
+// in [2^b, 2^(b+1)) and no t/u is a tie, every step adds the integer rint(t/u)
+// to M, and integers < 2^53 add exactly in any order, so a run of terms is a
+// DPP scan; a tie (t/u = k + 1/2) steps by k or k + 1 whichever makes M even,
+// settled tie by tie in order after the scan.  A round scans the next 64 terms
+// at the unit of C's binade, keeps the values up to the first term that leaves
+// the binade or is not >= 0, adds that term with an ordinary FP64 add (the
+// reference's own operation) and starts the next round after it.  One wave is latency-bound:
+// a round costs ~500 cycles, the one-lane loop ~30 per term (more rows per
+// round were measured slower: tools/sum_bench.hip).  Every lane of the wave
+// calls it with the same arguments; out may be null (only the total is
+// wanted); *stop (if given) is polled once per round: when set, the sum is
+// abandoned and *stopped set.
+namespace wseq {
+__device__ __forceinline__ int expo(double x) {  // biased exponent (sign set: >= 2048)
+    return (int)((unsigned long long)__double_as_longlong(x) >> 52);
+}
+__device__ __forceinline__ double p2(int biased) {  // 2^(biased - 1023), 1 <= biased <= 2046
+    return __longlong_as_double((long long)((unsigned long long)biased << 52));
+}
+}  // namespace wseq
+
+__device__ __forceinline__ double wave_seq_sum(const double *t, int cnt, double C, double *out, int lane,
+                                               const int *stop, bool *stopped) {
+    using namespace wseq;
+    int pos = 0;
+    double tv = lane < cnt ? t[lane] : 0.0;  // the window [pos, pos + 64)
+    while (pos < cnt) {
+        const int lim = min(64, cnt - pos);
+        // the next window, if this round keeps all 64 terms
+        const double tn = pos + 64 + lane < cnt ? t[pos + 64 + lane] : 0.0;
+        if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            *stopped = true;
+            return C;
+        }
+        const int eb = expo(C);
+        int f;  // first term off the run
+        double Ci = C;
+        if (eb < 64 || eb > 2000) {  // 0, tiny, huge, inf, NaN or negative: one plain step
+            f = 0;
+        } else {
+            const double u = p2(eb - 52), top = p2(eb + 1);
+            const bool act = lane < lim;  // (bitwise & |: no branches)
+            const double x = act ? tv * p2(2098 - eb) : 0.0;  // t/u, exact
+            const double fl = __builtin_floor(x);
+            const bool tie = act & (x - fl == 0.5);
+            // ties step by floor(x) first; each is then rounded to even in order below
+            Ci = C + wave_scan_f64(tie ? fl : __builtin_rint(x)) * u;  // exact below top
+            unsigned long long ties = __ballot(tie);
+            while (ties) {  // (M + k) + 1/2 rounds to the even one of M + k, M + k + 1
+                const int l = __builtin_ctzll(ties);
+                ties &= ties - 1;
+                const unsigned lo32 = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)__double_as_longlong(Ci), l);
+                if (lo32 & 1u) Ci = lane >= l ? Ci + u : Ci;  // odd: one unit up from lane l on
+            }
+            const unsigned long long bad = __ballot(act & (!(tv >= 0.0) | !(Ci < top)));
+            f = bad ? __builtin_ctzll(bad) : lim;
+            if (out && lane < f) out[pos + lane] = Ci;
+        }
+        if (f < lim) {
+            C = (f > 0 ? readlane_f64(Ci, f - 1) : C) + readlane_f64(tv, f);  // the reference's add
+            if (out && lane == 0) out[pos + f] = C;
+            pos += f + 1;
+            tv = pos + lane < cnt ? t[pos + lane] : 0.0;
+        } else {
+            C = readlane_f64(Ci, lim - 1);
+            pos += lim;
+            tv = tn;
+        }
+    }
+    return C;
 }
 
 }  // namespace tdstar

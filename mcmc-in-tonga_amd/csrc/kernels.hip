@@ -164,12 +164,12 @@ __global__ __launch_bounds__(256) void k_ray_sums(const int *__restrict__ ray_of
 
 // ---------------------------------------------------------------------------
 // Stage 3: chi^2, MCsub.jl:169-172, strictly sequential in k.  Terms in
-// parallel, then either one lane adds them in k order (short sums) or the
-// block reproduces that order exactly with binade-segmented integer scans
-// (exact_sum.h; long sums), falling back to the one lane if a guess fails.
+// parallel, then the k-order sum reproduced exactly with binade-segmented
+// integer scans (exact_sum.h): by the block for long sums, by one wave for
+// short ones and whenever the block's guess fails.
 // ---------------------------------------------------------------------------
 constexpr int kChi2Threads = 1024;
-constexpr int kExactMinTerms = 2048;  // below: the one-lane loop is as fast
+constexpr int kExactMinTerms = 2048;  // below: the one-wave sum is as fast
 
 __global__ __launch_bounds__(kChi2Threads) void k_chi2(const double *__restrict__ ptS,
                                                        const double *__restrict__ tS,
@@ -185,21 +185,11 @@ __global__ __launch_bounds__(kChi2Threads) void k_chi2(const double *__restrict_
     double C = 0.0;
     bool done = false;
     if (n >= kExactMinTerms) done = block_exact_sum<kChi2Threads>(terms, n, 0.0, nullptr, &C, w);
-    if (threadIdx.x == 0) {
-        if (!done) {
-            C = 0.0;
-            int k = 0;
-            for (; k + 8 <= n; k += 8) {
-                double t[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) t[u] = terms[k + u];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) C = C + t[u];
-            }
-            for (; k < n; ++k) C = C + terms[k];
-        }
-        *phi = C;
+    if (!done && threadIdx.x < 64) {  // one wave, the same left-to-right sum (exact_sum.h)
+        bool stopped = false;
+        C = wave_seq_sum(terms, n, 0.0, nullptr, (int)threadIdx.x, nullptr, &stopped);
     }
+    if (threadIdx.x == 0) *phi = C;
 }
 
 __global__ __launch_bounds__(kChi2Threads) void k_test_exact_sum(const double *__restrict__ term, int cnt, double C0,
@@ -214,7 +204,23 @@ __global__ __launch_bounds__(kChi2Threads) void k_test_exact_sum(const double *_
     }
 }
 
+__global__ __launch_bounds__(64) void k_test_wave_seq_sum(const double *__restrict__ term, int cnt, double C0,
+                                                          double *__restrict__ prefix, double *C_end,
+                                                          int *fallbacks) {
+    bool stopped = false;
+    const double C = wave_seq_sum(term, cnt, C0, prefix, (int)threadIdx.x, nullptr, &stopped);
+    if (threadIdx.x == 0) {
+        *C_end = C;
+        *fallbacks = 0;
+    }
+}
+
 }  // namespace
+
+hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fallbacks) {
+    hipLaunchKernelGGL(k_test_wave_seq_sum, dim3(1), dim3(64), 0, nullptr, term, cnt, C0, prefix, C_end, fallbacks);
+    return hipGetLastError();
+}
 
 hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast) {
     hipLaunchKernelGGL(k_test_exact_sum, dim3(1), dim3(kChi2Threads), 0, nullptr, term, cnt, C0, prefix, C_end, fast);

@@ -5,6 +5,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace tdstar {
 
 // ---- cross-lane reductions on 64-bit keys through DPP (VALU, no LDS) ----
@@ -46,6 +48,27 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// inclusive prefix sum over the 64 lanes (lane l: v_0 + ... + v_l, in a tree
+// association: exact when every value and partial sum is an integer < 2^53).
+// The row shifts zero-fill (bound_ctrl); the row broadcasts leave the
+// unselected rows at `old` = 0.
+__device__ __forceinline__ double wave_scan_f64(double v) {
+    auto shr = [](double a, auto ctrl) {
+        const unsigned long long b = (unsigned long long)__double_as_longlong(a);
+        const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, decltype(ctrl)::value, 0xf, 0xf, true);
+        const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), decltype(ctrl)::value, 0xf, 0xf, true);
+        return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    };
+    auto bits = [](double a) { return (unsigned long long)__double_as_longlong(a); };
+    v = v + shr(v, std::integral_constant<int, 0x111>{});  // row_shr 1, 2, 4, 8: scan inside rows of 16
+    v = v + shr(v, std::integral_constant<int, 0x112>{});
+    v = v + shr(v, std::integral_constant<int, 0x114>{});
+    v = v + shr(v, std::integral_constant<int, 0x118>{});
+    v = v + __longlong_as_double((long long)dpp_u64<0x142, 0xa>(bits(v), 0ull));  // row_bcast:15 -> rows 1, 3
+    v = v + __longlong_as_double((long long)dpp_u64<0x143, 0xc>(bits(v), 0ull));  // row_bcast:31 -> rows 2, 3
+    return v;
 }
 
 // sum over the 64 lanes (any association: for bounds, not for results), to every lane

@@ -31,13 +31,13 @@ def main():
     ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000, chain=1), tt.random_model(N, 3))
     ch.run(2000)
     L = tt.lib()
-    out0 = (ctypes.c_int64 * 16)()
+    out0 = (ctypes.c_int64 * 64)()
     L.tdt_chain_profile(ch.h, 1, out0)
     st0 = ch.stats()
     t0 = time.perf_counter()
     ch.run(iters)
     el = time.perf_counter() - t0
-    out = (ctypes.c_int64 * 16)()
+    out = (ctypes.c_int64 * 64)()
     L.tdt_chain_profile(ch.h, 0, out)
     cyc = np.array(out[:7], dtype=np.float64) - np.array(out0[:7], dtype=np.float64)
     cyc[6] += (out[12] - out0[12]) + (out[13] - out0[13])  # G = commit + next proposal + barrier
@@ -58,6 +58,13 @@ def main():
                "commit": round((out[12] - out0[12]) / iters, 1),
                "next proposal": round((out[13] - out0[13]) / iters, 1),
                "final barrier": round((out[6] - out0[6]) / iters, 1)}}
+    # the same phases split by action: cycles per proposal of that action
+    names = PHASES[:6] + ["G commit", "G next proposal", "final barrier"]
+    res["phases_by_action (cycles per proposal)"] = {
+        a: {names[j]: round((out[16 + 10 * i + j] - out0[16 + 10 * i + j]) / max(prop[i], 1), 1) for j in range(9)}
+        for i, a in enumerate(["birth", "death", "change", "move"])}
+    res["F per wave (cycles per iter): chi2 scan, next proposal, tile maxima x4, bound, grid prefetch"] = [
+        round((out[56 + w] - out0[56 + w]) / iters, 1) for w in range(8)]
     print(json.dumps(res, indent=1))
 
 

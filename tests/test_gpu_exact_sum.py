@@ -1,14 +1,18 @@
-"""GPU: the block-wide exact sequential sum (exact_sum.h) behind chi^2 over
-long ray lists must equal the strictly left-to-right FP64 loop of
-MCsub.jl:170-172 bit for bit whenever it claims success, and claim success
-on realistic data.  Reference: a Python loop of IEEE-754 double adds (the
-same operation sequence as the Julia loop)."""
+"""GPU: the exact sequential sums of exact_sum.h behind chi^2 -- the
+block-wide one (long ray lists) and the one-wave one (the chain's tails) --
+must equal the strictly left-to-right FP64 loop of MCsub.jl:170-172 bit for
+bit whenever they claim success, and claim success on realistic data (the
+one-wave sum always does).  Reference: a Python loop of IEEE-754 double adds
+(the same operation sequence as the Julia loop)."""
 import ctypes
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+
+WAVE_FALLBACKS = []  # chunks of the one-wave sum that took its slow path, per call
 
 
 def seq(terms, c0):
@@ -19,25 +23,37 @@ def seq(terms, c0):
     return np.array(out)
 
 
-def run(tt, terms, c0):
+def run(tt, terms, c0, wave=False):
     terms = np.ascontiguousarray(terms, dtype=np.float64)
     pre = np.zeros(len(terms))
     ce = ctypes.c_double()
-    fast = ctypes.c_int()
+    fast = ctypes.c_int(1)
     P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
-    assert tt.lib().tdt_exact_sum(0, P(terms), len(terms), float(c0), P(pre), ctypes.byref(ce),
-                                  ctypes.byref(fast)) == 0
+    if wave:
+        fb = ctypes.c_int()
+        assert tt.lib().tdt_wave_seq_sum(0, P(terms), len(terms), float(c0), P(pre), ctypes.byref(ce),
+                                         ctypes.byref(fb)) == 0
+        WAVE_FALLBACKS.append(fb.value)
+    else:
+        assert tt.lib().tdt_exact_sum(0, P(terms), len(terms), float(c0), P(pre), ctypes.byref(ce),
+                                      ctypes.byref(fast)) == 0
     return bool(fast.value), pre, ce.value
 
 
 def check(tt, terms, c0):
-    fast, pre, ce = run(tt, terms, c0)
-    if fast:
-        want = seq(terms, c0)
-        bad = np.nonzero(pre != want)[0]
-        assert len(bad) == 0, (bad[:5], pre[bad[:5]], want[bad[:5]])
-        assert ce == want[-1]
-    return fast
+    """Both sums; returns whether the block-wide one took its fast path."""
+    want = seq(terms, c0)
+    for wave in (False, True):
+        fast, pre, ce = run(tt, terms, c0, wave)
+        if fast:
+            same = (pre == want) | (np.isnan(pre) & np.isnan(want))
+            bad = np.nonzero(~same)[0]
+            assert len(bad) == 0, (wave, bad[:5], pre[bad[:5]], want[bad[:5]])
+            assert ce == want[-1] or (np.isnan(ce) and np.isnan(want[-1])), wave
+        assert fast or not wave
+        if not wave:
+            block_fast = fast
+    return block_fast
 
 
 def test_chi2_like_terms(tt):
@@ -82,3 +98,20 @@ def test_adversarial(tt):
         check(tt, np.exp(rng.uniform(-40, 40, 3000)), float(rng.uniform(0, 10)))
     # sums landing exactly on powers of two
     check(tt, np.concatenate([[0.5, 0.25, 0.25, 1.0, 2.0, 4.0 - 2.0 ** -50, 2.0 ** -50], np.ones(2000)]), 0.0)
+
+
+def test_wave_sum_binade_walk(tt):
+    """The chain's case: ~381 chi^2-like terms from every starting prefix
+    (zero, small, one binade below the top), with NaN/inf/negative terms."""
+    rng = np.random.default_rng(11)
+    base = rng.exponential(36.0, 381)
+    del WAVE_FALLBACKS[:]
+    for k0 in (0, 1, 17, 190, 380):
+        c0 = float(seq(base[:k0], 0.0)[-1]) if k0 else 0.0
+        check(tt, base[k0:], c0)
+    assert WAVE_FALLBACKS == [0, 0, 0, 0, 0], WAVE_FALLBACKS
+    check(tt, np.concatenate([base[:50], [np.inf], base[50:80]]), 3.0)
+    check(tt, np.concatenate([base[:50], [-2.5], base[50:80]]), 3.0)
+    check(tt, np.concatenate([base[:70], [np.nan], base[70:90]]), 3.0)
+    check(tt, np.full(130, 2.0 ** 60), 2.0 ** 62)            # huge, exact ties
+    check(tt, rng.exponential(1e-300, 200), 1e-310)            # subnormal start
