@@ -264,8 +264,8 @@ def full_evaluate(tt, ctx, model, N, reps=50):
     cells = model.cells()
     E = ctx.P * N
     out = {}
-    kernels = {"grid": ["nn_grid_build", "nn_grid", "nn_fallback", "ray_sums", "chi2"],
-               "brute_force": ["nn_partial", "nn_merge", "ray_sums", "chi2"]}
+    kernels = {"grid": ["nn_grid_build", "nn_grid", "ray_sums_chi2"],
+               "brute_force": ["nn_partial", "nn_merge", "ray_sums_chi2"]}
     for name, method in (("grid", ctx.NN_GRID), ("brute_force", ctx.NN_BRUTE)):
         ctx.set_nn_method(method)
         for _ in range(3):

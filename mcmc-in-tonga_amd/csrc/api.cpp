@@ -128,9 +128,15 @@ int ensure_cells(td_ctx *ctx, int64_t ncells) {
     ctx->h_cells = nullptr;
     ctx->cell_cap = 0;
     TD_HIP(ctx, hipMalloc(&ctx->cells, sizeof(double) * 4 * (size_t)cap));
-    TD_HIP(ctx, hipHostMalloc(&ctx->h_cells, sizeof(double) * 4 * (size_t)cap, hipHostMallocDefault));
+    TD_HIP(ctx, hipHostMalloc(&ctx->h_cells, sizeof(double) * 4 * (size_t)cap,
+                              hipHostMallocMapped | hipHostMallocNonCoherent));
+    TD_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->h_cells_dev), ctx->h_cells, 0));
     ctx->cell_cap = cap;
     return TD_OK;
+}
+
+bool uses_grid(const td_ctx *ctx, int64_t ncells) {
+    return ncells > 0 && (ctx->nn_method == 2 || (ctx->nn_method == 0 && ncells >= kGridMinCells));
 }
 
 int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
@@ -142,21 +148,25 @@ int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z,
     const int64_t s = ncells;
     ctx->cell_stride = s;
     double *h = ctx->h_cells;
-    std::memcpy(h, x, sizeof(double) * (size_t)ncells);
-    std::memcpy(h + s, y, sizeof(double) * (size_t)ncells);
-    std::memcpy(h + 2 * s, z, sizeof(double) * (size_t)ncells);
-    std::memcpy(h + 3 * s, zeta, sizeof(double) * (size_t)ncells);
     const double *src[3] = {x, y, z};
-    for (int a = 0; a < 3; ++a) {  // box of the cells for the bucket grid
+    for (int a = 0; a < 3; ++a) {  // staged, and the box of the cells for the bucket grid, in one pass
         double lo = HUGE_VAL, hi = -HUGE_VAL;
+        double *dst = h + a * s;
         for (int64_t i = 0; i < ncells; ++i) {
             const double v = src[a][i];
+            dst[i] = v;
             lo = v < lo ? v : lo;  // NaN compares false: skipped
             hi = v > hi ? v : hi;
         }
         ctx->cell_lo[a] = lo <= hi ? lo : 0.0;
         ctx->cell_hi[a] = lo <= hi ? hi : 0.0;
     }
+    std::memcpy(h + 3 * s, zeta, sizeof(double) * (size_t)ncells);
+    if (uses_grid(ctx, ncells)) {  // the grid build reads the staged cells itself (no DMA copy)
+        ctx->cells_stage = ctx->h_cells_dev;
+        return TD_OK;
+    }
+    ctx->cells_stage = nullptr;
     TD_HIP(ctx, hipMemcpyAsync(ctx->cells, h, sizeof(double) * 4 * (size_t)ncells, hipMemcpyHostToDevice,
                                ctx->stream));
     return TD_OK;
@@ -166,11 +176,12 @@ hipError_t nearest_uploaded(td_ctx *ctx, const double *qx, const double *qy, con
                             int64_t qy_stride, int64_t qz_stride, int64_t ncells, int *best_i, double *best_d,
                             double *zeta0) {
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
-    const bool grid = ctx->nn_method == 2 || (ctx->nn_method == 0 && ncells >= kGridMinCells);
-    if (grid && ncells > 0) {
+    if (uses_grid(ctx, ncells)) {
         const CellGrid G = make_cell_grid(ctx->cell_lo, ctx->cell_hi, (double)ncells / 2.0, 4096, kGridMaxBuckets);
+        const double *stage = ctx->cells_stage;
+        ctx->cells_stage = nullptr;  // copied by this search's grid build
         return launch_nearest_grid(qx, qy, qz, npts, qy_stride, qz_stride, ctx->cells, ctx->cell_stride, ncells, G,
-                                   ctx->nn, ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm);
+                                   ctx->nn, ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm, stage);
     }
     return launch_nearest(qx, qy, qz, npts, qy_stride, qz_stride, ctx->cells, ctx->cell_stride, ncells, ctx->nn,
                           ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm);
@@ -186,9 +197,9 @@ void free_ctx(td_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->timer.release();
-    void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->cells,
+    void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->g.done, c->cells,
                    c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->phi,
-                   c->q, c->q_i, c->q_z, c->chain_desc, c->nn.g_count, c->nn.g_ent, c->nn.g_fb, c->raster, c->raster_i};
+                   c->q, c->q_i, c->q_z, c->chain_desc, c->nn.g_count, c->nn.g_ent, c->raster, c->raster_i};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     void *host[] = {c->h_cells, c->h_out, c->h_best_i, c->h_q, c->h_q_i, c->h_q_z, c->h_chain_desc};
@@ -298,6 +309,8 @@ int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, 
     rc = rc ? rc : dalloc((void **)&c->g.tS, nb, "hipMalloc(tS)");
     rc = rc ? rc : dalloc((void **)&c->g.sig, nb, "hipMalloc(sig)");
     rc = rc ? rc : dalloc((void **)&c->g.terms, nb, "hipMalloc(terms)");
+    rc = rc ? rc : dalloc((void **)&c->g.done, sizeof(unsigned), "hipMalloc(done)");
+    if (!rc && hipMemset(c->g.done, 0, sizeof(unsigned)) != hipSuccess) rc = hip_err(c, hipErrorUnknown, "hipMemset(done)");
     rc = rc ? rc : dalloc((void **)&c->best_i, sizeof(int) * (size_t)(P > 0 ? P : 1), "hipMalloc(best_i)");
     rc = rc ? rc : dalloc((void **)&c->best_d, Pb, "hipMalloc(best_d)");
     rc = rc ? rc : dalloc((void **)&c->zeta0, Pb, "hipMalloc(zeta0)");
@@ -305,8 +318,10 @@ int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, 
     rc = rc ? rc : dalloc((void **)&c->phi, sizeof(double) * (size_t)(n + 1), "hipMalloc(phi, ptS)");
     if (!rc) c->ptS = c->phi + 1;
     if (rc) return fail(rc);
-    e = hipHostMalloc(&c->h_out, sizeof(double) * (size_t)(n + 1), hipHostMallocDefault);
+    e = hipHostMalloc(&c->h_out, sizeof(double) * (size_t)(n + 1), hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) return fail(hip_err(c, e, "hipHostMalloc(out)"));
+    e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->h_out_dev), c->h_out, 0);
+    if (e != hipSuccess) return fail(hip_err(c, e, "hipHostGetDevicePointer(out)"));
     e = hipHostMalloc(&c->h_best_i, sizeof(int) * (size_t)(P > 0 ? P : 1), hipHostMallocDefault);
     if (e != hipSuccess) return fail(hip_err(c, e, "hipHostMalloc(best_i)"));
 
@@ -376,12 +391,9 @@ int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const dou
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
     hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, nCells, ctx->best_i, ctx->best_d, ctx->zeta0);
     if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
-    e = launch_ray_sums(g, ctx->zeta0, ctx->ptS, ctx->stream, tm);
-    if (e != hipSuccess) return hip_err(ctx, e, "ray-sum kernel");
-    e = launch_chi2(g, ctx->ptS, ctx->phi, ctx->stream, tm);
-    if (e != hipSuccess) return hip_err(ctx, e, "chi2 kernel");
-    TD_HIP(ctx, hipMemcpyAsync(ctx->h_out, ctx->phi, sizeof(double) * (size_t)(g.n + 1), hipMemcpyDeviceToHost,
-                               ctx->stream));
+    // [phi, ptS] land in pinned host memory straight from the kernel (no copy back)
+    e = launch_ray_sums_chi2(g, ctx->zeta0, ctx->ptS, ctx->phi, ctx->stream, tm, ctx->h_out_dev);
+    if (e != hipSuccess) return hip_err(ctx, e, "ray-sum / chi2 kernel");
     if (nearest_out && g.P)
         TD_HIP(ctx, hipMemcpyAsync(ctx->h_best_i, ctx->best_i, sizeof(int) * (size_t)g.P, hipMemcpyDeviceToHost,
                                    ctx->stream));

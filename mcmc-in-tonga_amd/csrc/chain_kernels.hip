@@ -131,7 +131,8 @@ struct Shared {
     long long proposed[5], accepted[5];
     double phi;
     int ncells, nslots, nfree;
-    double lnN[3];  // logN[ncells - 1 .. ncells + 1]
+    double lnN[3];     // logN[ncells - 1 .. ncells + 1]
+    double lnN_far[2];  // logN[ncells - 2], logN[ncells + 2]: read during phase F for a birth/death commit
     double q_zeta;         // result of the birth/death Interpolation query
     int grid_fallbacks32;  // grid searches that needed the full scan
     int grid_ovf;          // LDS copy of *d.grid_overflow
@@ -556,8 +557,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     }
     __syncthreads();
 
+    // wave 0 lane 0 decides, commits and proposes: the scalars only it changes
+    // live in its registers (LDS copies are written, never read back on its path)
+    const long long iter0 = sh.iter;
+    double phi_r = sh.phi;
+    int cur_r = 0;
     for (long long it = 0; it < iters; ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
+        bool acc_r = false;
         const PState &cur = sh.ps[sh.cur];
         const Proposal p = cur.p;
         const int action = p.action;
@@ -726,26 +733,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             }
             if (tid == 0) {
                 const int k0 = sh.k0;
-                if (fwd) {
-                    sh.evaluations += 1;
-                    // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
-                    // candidate points (coords + cached slot/distance, 36 B), grid queries
-                    // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
-                    // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
-                    sh.bytes += (long long)NT * 32 + (long long)sh.pts_seen * 36 +
-                                (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
-                                (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28;
-                }
                 // Metropolis-Hastings decision (a proven rejection skips the rest of the sum:
                 // accept() on the exact phi_n would reject too)
                 const bool early = fwd && k0 < n && sh.early_reject;
-                if (prof_on && early) sh.prof[14] += 1;  // diagnostic: proven rejections
-                const bool acc = !early && tdchain::accept(P, pp, sh.phi, phi_n, czeta, zeta_killed,
+                const bool acc = !early && tdchain::accept(P, pp, phi_r, phi_n, czeta, zeta_killed,
                                                            zetanew_death, sh.lnN);
+                acc_r = acc;
                 sh.accept = acc ? 1 : 0;
                 sh.phi_n = phi_n;
                 if (acc) {
-                    sh.accepted[action] += 1;
                     sh.g_op = action == tdchain::kBirth ? 2 : action == tdchain::kDeath ? 1
                               : action == tdchain::kMove ? 3 : 0;
                     sh.g_slot = action == tdchain::kBirth ? new_slot : slot_k;
@@ -755,6 +751,20 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.g_nx = pp.x;
                     sh.g_ny = pp.y;
                     sh.g_nz = pp.z;
+                    atomicAdd((unsigned long long *)&sh.accepted[action], 1ull);
+                }
+                // accounting, off the decision's path (no-return LDS atomics)
+                if (prof_on && early) atomicAdd((unsigned long long *)&sh.prof[14], 1ull);  // proven rejections
+                if (fwd) {
+                    atomicAdd((unsigned long long *)&sh.evaluations, 1ull);
+                    // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
+                    // candidate points (coords + cached slot/distance, 36 B), grid queries
+                    // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
+                    // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
+                    atomicAdd((unsigned long long *)&sh.bytes,
+                              (unsigned long long)((long long)NT * 32 + (long long)sh.pts_seen * 36 +
+                                                   (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
+                                                   (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28));
                 }
             } else if (tid == 64) {  // the next proposal as if this one were rejected
                 if (can_spec) {
@@ -767,6 +777,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     grid_prefetch(d, sh, lane, action, action == tdchain::kBirth ? new_slot : slot_k, kx, ky,
                                   kz, pp.x, pp.y, pp.z);
             } else if (wv == kWaves - 2) {
+                if (lane == 0 && (action == tdchain::kBirth || action == tdchain::kDeath)) {
+                    sh.lnN_far[0] = d.logN[max(ncells - 2, 0)];
+                    sh.lnN_far[1] = d.logN[ncells + 2];
+                }
                 // a lower bound of phi_n from all new terms: the sequential sum of n
                 // non-negative terms is within n ulps of any other association; above
                 // the rejection bound by a wide margin, the proposal is rejected
@@ -844,13 +858,19 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         else
                             sh.nslots += 1;
                         sh.ncells = ncells + 1;
-                        for (int k = 0; k < 3; ++k) sh.lnN[k] = d.logN[ncells + k];
+                        const double a = sh.lnN[1], b = sh.lnN[2], c = sh.lnN_far[1];
+                        sh.lnN[0] = a;
+                        sh.lnN[1] = b;
+                        sh.lnN[2] = c;
                     } else if (action == tdchain::kDeath) {
                         d.free_slots[sh.nfree] = sk;
                         sh.nfree += 1;
                         d.rank[sk] = -1;
                         sh.ncells = ncells - 1;
-                        for (int k = 0; k < 3; ++k) sh.lnN[k] = d.logN[ncells - 2 + k];
+                        const double a = sh.lnN_far[0], b = sh.lnN[0], c = sh.lnN[1];
+                        sh.lnN[0] = a;
+                        sh.lnN[1] = b;
+                        sh.lnN[2] = c;
                     } else if (action == tdchain::kChange) {
                         d.czeta[sk] = pp.zeta;
                     } else {
@@ -858,7 +878,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         d.cy[sk] = pp.y;
                         d.cz[sk] = pp.z;
                     }
-                    sh.phi = sh.phi_n;
+                    phi_r = sh.phi_n;
+                    sh.phi = phi_r;
                 }
             } else {  // rejected: flags down, the changed rays get their old chi^2 terms back
                 for (int c = tid; c < nc; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
@@ -872,33 +893,33 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         STAMP(12);
         // ===== end of iteration: the next proposal (wave 0; draws refilled every 64) =====
         if (wv == 0) {
-            if (lane == 0) {
-                if (prof_on) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
-                sh.iter += 1;
-            }
+            if (prof_on && lane == 0) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
             if (it + 1 < iters) {
                 if (((it + 1) & 63) == 0) {
                     wave_sync_lds();
-                    draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
+                    draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(iter0 + it + 1 + lane));
                     wave_sync_lds();
                 }
                 if (lane == 0) {
-                    const bool acc = sh.accept != 0;
+                    const bool acc = acc_r;
                     // the guess holds unless an accepted proposal changed what it read
+                    const PState &g = sh.ps[cur_r ^ 1];
                     const bool keep = sh.spec_ok && can_spec &&
                                       (!acc || ((action == tdchain::kChange || action == tdchain::kMove) &&
-                                                sh.ps[sh.cur ^ 1].slot_k != slot_k));
+                                                g.slot_k != slot_k));
                     if (keep) {
-                        sh.cur ^= 1;  // adopt the guess: no copy
+                        cur_r ^= 1;  // adopt the guess: no copy
+                        sh.cur = cur_r;
                     } else {
                         // a just-killed position: later positions read the pre-shift order
                         const int killed = (acc && action == tdchain::kDeath) ? (int)pp.index : -1;
-                        make_proposal(sh.ps[sh.cur], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots, d.free_slots,
+                        make_proposal(sh.ps[cur_r], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots, d.free_slots,
                                       d.cx, d.cy, d.cz, d.czeta, [&](int pos) {
                                           return (killed >= 0 && pos >= killed) ? d.order_tmp[pos + 1] : v.ord[pos];
                                       });
                     }
-                    if (sh.ps[sh.cur].p.active) sh.proposed[sh.ps[sh.cur].p.action] += 1;
+                    const tdchain::Proposal &np = sh.ps[cur_r].p;
+                    if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
                     sh.spec_ok = 0;
                     sh.early_reject = 0;
                     sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
@@ -924,7 +945,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     }
     if (tid == 0) {
         ChainScalars &s = *d.st;
-        s.iter = sh.iter;
+        s.iter = iter0 + iters;
         s.evaluations += sh.evaluations;
         s.bytes += sh.bytes;
         for (int a = 0; a < 5; ++a) {

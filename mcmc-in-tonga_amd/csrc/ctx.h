@@ -24,6 +24,8 @@ struct td_ctx {
     double *cells = nullptr;
     int64_t cell_stride = 1;            // SoA stride of the uploaded cells (= their count)
     double *h_cells = nullptr;
+    double *h_cells_dev = nullptr;      // the same pinned buffer, as the device addresses it
+    const double *cells_stage = nullptr;  // non-null: the device copy is still to be made (from here)
     int64_t cell_cap = 0;
 
     // per-evaluation outputs / caches
@@ -33,7 +35,8 @@ struct td_ctx {
     double *zeta0 = nullptr;
     double *ptS = nullptr;
     double *phi = nullptr;
-    double *h_out = nullptr;            // pinned: [phi, ptS[n]]
+    double *h_out = nullptr;            // pinned: [phi, ptS[n]], written by the evaluate kernel
+    double *h_out_dev = nullptr;        // the same, as the device addresses it
     int *h_best_i = nullptr;            // pinned [P]
 
     // query points for td_interpolate
@@ -72,6 +75,8 @@ int hip_err(td_ctx *ctx, hipError_t e, const char *what);
 // Make room for `ncells` cells (device + pinned staging).
 int ensure_cells(td_ctx *ctx, int64_t ncells);
 // Pack cells into the pinned staging buffer and upload them (async on ctx->stream).
+// the bucket-grid search (else brute force) for this many cells
+bool uses_grid(const td_ctx *ctx, int64_t ncells);
 int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                  int64_t ncells);
 // Nearest cell of npts query points against the uploaded cells (brute force

@@ -383,6 +383,23 @@ __device__ __forceinline__ double wave_seq_sum(const double *t, int cnt, double 
             C = (f > 0 ? readlane_f64(Ci, f - 1) : C) + readlane_f64(tv, f);  // the reference's add
             if (out && lane == 0) out[pos + f] = C;
             pos += f + 1;
+            if (f < 16 && pos + 16 <= cnt) {  // short runs (small sums cross binades often): plain adds
+                double tt[16], cc[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) tt[u] = t[pos + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    C = C + tt[u];
+                    cc[u] = C;
+                }
+                if (out && lane < 16) {
+                    double o = cc[0];
+#pragma unroll
+                    for (int u = 1; u < 16; ++u) o = lane == u ? cc[u] : o;
+                    out[pos + lane] = o;
+                }
+                pos += 16;
+            }
             tv = pos + lane < cnt ? t[pos + lane] : 0.0;
         } else {
             C = readlane_f64(Ci, lim - 1);

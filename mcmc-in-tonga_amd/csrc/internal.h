@@ -103,10 +103,11 @@ struct NNWork {
     double *part_d = nullptr;  // [chunks][npts]
     int *part_i = nullptr;
     size_t cap = 0;            // elements
-    int *g_count = nullptr;        // [buckets] cells per bucket
+    int *g_count = nullptr;        // [2][buckets] cells per bucket: two sets, alternate searches
     BucketEntry *g_ent = nullptr;  // [buckets][kGridCap] entries {x, y, z, cell index}
-    int *g_fb = nullptr;           // [npts] points left to the brute force, then their count
-    size_t g_count_cap = 0, g_ent_cap = 0, g_fb_cap = 0;  // bytes
+    size_t g_count_cap = 0, g_ent_cap = 0;  // bytes (g_count: both sets)
+    int g_par = 0;                 // the set the next search fills (zero)
+    int64_t g_used[2] = {0, 0};    // buckets each set holds counts in (zeroed by the other's search)
 };
 
 struct Geometry {
@@ -115,6 +116,7 @@ struct Geometry {
     int *ray_off = nullptr;
     double *tS = nullptr, *sig = nullptr;
     double *terms = nullptr;  // [n] scratch: chi^2 terms of one evaluation
+    unsigned *done = nullptr;  // workgroups of the ray-sum launch that finished (0 between launches)
 };
 
 // How a cell set is split over workgroups for the brute-force search.
@@ -138,10 +140,13 @@ hipError_t launch_nearest(const double *qx, const double *qy, const double *qz, 
 // Same result as launch_nearest through a bucket grid G over the cells (which
 // must all lie in G's box; G.gx*G.gy*G.gz <= kGridMaxBuckets, ncells >= 1).
 // Cells are ordered by nothing but their index: ties resolve exactly.
+// stage (optional): the cells in pinned host memory; the grid build then
+// also writes them to `cells` (one pass over PCIe instead of a DMA copy)
 hipError_t launch_nearest_grid(const double *qx, const double *qy, const double *qz, int64_t npts,
-                               int64_t qy_stride, int64_t qz_stride, const double *cells, int64_t stride,
+                               int64_t qy_stride, int64_t qz_stride, double *cells, int64_t stride,
                                int64_t ncells, const CellGrid &G, NNWork &work, int num_cus, int *best_i,
-                               double *best_d, double *zeta0, hipStream_t s, Timer *tm = nullptr);
+                               double *best_d, double *zeta0, hipStream_t s, Timer *tm = nullptr,
+                               const double *stage = nullptr);
 
 // Testing: the block-wide exact sequential sum (exact_sum.h) on device buffers.
 hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fallbacks);
@@ -151,6 +156,8 @@ hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix
 hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm = nullptr);
 
 // phi = sequential sum_k ((ptS-tS)^2*1.0)/sig^2 (MCsub.jl:169-172).
-hipError_t launch_chi2(const Geometry &g, const double *ptS, double *phi, hipStream_t s, Timer *tm = nullptr);
+// per-ray t* (launch_ray_sums) and chi^2 into *phi in one launch
+hipError_t launch_ray_sums_chi2(const Geometry &g, const double *zeta0, double *ptS, double *phi, hipStream_t s,
+                                Timer *tm = nullptr, double *host_out = nullptr);
 
 }  // namespace tdstar

@@ -6,15 +6,17 @@
 // distance, cell index) over all cells, among distances below the 1e9
 // sentinel -- v_nearest's strict '<' scan in index order keeps the FIRST
 // minimum.  The grid only decides where to look:
-//   k_grid_fill    one lane per cell: append {x, y, z, index} to its bucket
-//                  (kGridCap entries; a fuller bucket is flagged);
-//   k_nn_grid      32 lanes per point, one per bucket of the 3x3x3 block
-//                  around it, DPP reduction; the answer counts only if it is
-//                  strictly closer than every face of the block
-//                  (grid_block_lb), i.e. than every cell outside, and no
-//                  bucket of the block overflowed -- else the point goes on a
-//                  list;
-//   k_nn_fallback  one wave per listed point: all cells (brute force).
+//   k_grid_fill  one lane per cell: append {x, y, z, index} to its bucket
+//                (kGridCap entries; a fuller bucket is flagged);
+//   k_nn_grid    32 lanes per point, one per bucket of the 3x3x3 block
+//                around it, DPP reduction; the answer counts only if it is
+//                strictly closer than every face of the block
+//                (grid_block_lb), i.e. than every cell outside, and no bucket
+//                of the block overflowed -- else the 5x5x5 block, else (rare)
+//                the same 32 lanes scan every cell.
+// Two launches per search: the bucket counts come in two sets used by
+// alternate searches, and each search's k_nn_grid zeroes the other set for
+// the next one (no memset, no third kernel).
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -46,13 +48,26 @@ __device__ __forceinline__ void take(double d, int i, double &bd, int &bi) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_grid_fill(const double *__restrict__ cells, int stride, int ncells,
-                                                   CellGrid G, int *__restrict__ count,
-                                                   BucketEntry *__restrict__ ent, int *__restrict__ fb_count) {
+__global__ __launch_bounds__(256) void k_grid_fill(double *__restrict__ cells, const double *__restrict__ stage,
+                                                   int stride, int ncells, CellGrid G, int *__restrict__ count,
+                                                   BucketEntry *__restrict__ ent) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *fb_count = 0;  // the fallback list of this search starts empty
     if (i >= ncells) return;
-    const double x = cells[i], y = cells[stride + i], z = cells[2 * stride + i];
+    double x, y, z;
+    if (stage) {  // the cells straight from pinned host memory, and the device copy on the way
+        x = stage[i];
+        y = stage[stride + i];
+        z = stage[2 * stride + i];
+        const double ze = stage[3 * stride + i];
+        cells[i] = x;
+        cells[stride + i] = y;
+        cells[2 * stride + i] = z;
+        cells[3 * stride + i] = ze;
+    } else {
+        x = cells[i];
+        y = cells[stride + i];
+        z = cells[2 * stride + i];
+    }
     const int b = grid_bucket(G, x, y, z);
     const int pos = atomicAdd(&count[b], 1);  // order inside a bucket does not matter
     if (pos < kGridCap) ent[(long)b * kGridCap + pos] = BucketEntry{x, y, z, i, 0};
@@ -84,20 +99,27 @@ __device__ __forceinline__ void half_min(double &d, int &i) {
 __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, const double *__restrict__ qy,
                                                  const double *__restrict__ qz, int npts, int ys, int zs, CellGrid G,
                                                  const int *__restrict__ count, const BucketEntry *__restrict__ ent,
-                                                 const double *__restrict__ zeta_cells, int *__restrict__ best_i,
-                                                 double *__restrict__ best_d, double *__restrict__ zeta0,
-                                                 int *__restrict__ fb_list, int *__restrict__ fb_count) {
+                                                 const double *__restrict__ cells, int stride, int ncells,
+                                                 int *__restrict__ best_i, double *__restrict__ best_d,
+                                                 double *__restrict__ zeta0, int *__restrict__ other_count,
+                                                 int other_nb) {
+    // the other set of bucket counts (the previous search's) is zeroed for the next search
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < other_nb; b += gridDim.x * blockDim.x) other_count[b] = 0;
     const int hl = threadIdx.x & 31;                             // lane in the half-wave
     const int p = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;  // one point per half-wave
     const int pc = min(p, npts - 1);                              // whole half-waves stay for the DPP
     const double x = qx[pc], y = qy[(long)pc * ys], z = qz[(long)pc * zs];
     const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
               bk = grid_axis(z, G.z0, G.iz, G.gz);
+    const double *zeta_cells = cells + 3 * (long)stride;
+    double bd = kSentinel;
+    int bx = INT_MAX;
+    bool proven = false;
     // the 3x3x3 block (one bucket per lane), then the 5x5x5 one (four per lane)
-    for (int R = 1; R <= 2; ++R) {
+    for (int R = 1; R <= 2 && !proven; ++R) {
         const int W = 2 * R + 1, nbk = W * W * W;
-        double bd = kSentinel;
-        int bx = INT_MAX;
+        bd = kSentinel;
+        bx = INT_MAX;
         bool over = false;
         for (int t = hl; t < nbk; t += 32) {
             const int ii = bi + t % W - R, jj = bj + (t / W) % W - R, kk = bk + t / (W * W) - R;
@@ -117,63 +139,29 @@ __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, 
         half_min(bd, bx);
         const unsigned long long ov = __ballot(over);
         const bool any_over = ((ov >> (threadIdx.x & 32)) & 0xffffffffull) != 0ull;
-        if (!any_over && bd < grid_block_lb(G, x, y, z, R)) {  // nothing outside can tie or win
-            if (hl == 0 && p < npts) {
-                const bool found = bd < kSentinel;
-                best_i[p] = found ? bx : -1;
-                if (best_d) best_d[p] = bd;
-                if (zeta0) zeta0[p] = found ? zeta_cells[bx] : 0.0;  // MCsub.jl:249
-            }
-            return;  // the whole half-wave: its point is answered
-        }
+        proven = !any_over && bd < grid_block_lb(G, x, y, z, R);  // nothing outside can tie or win
     }
-    if (hl == 0 && p < npts) fb_list[atomicAdd(fb_count, 1)] = p;
-}
-
-// One wave per listed point: every cell, lexicographic min over the lanes.
-__global__ __launch_bounds__(256) void k_nn_fallback(const double *__restrict__ qx, const double *__restrict__ qy,
-                                                     const double *__restrict__ qz, int ys, int zs,
-                                                     const int *__restrict__ fb_list, const int *__restrict__ fb_count,
-                                                     const double *__restrict__ cells, int stride, int ncells,
-                                                     int *__restrict__ best_i, double *__restrict__ best_d,
-                                                     double *__restrict__ zeta0, int *__restrict__ count, int nb) {
-    // the bucket counts are spent: leave them zero for the next search
-    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x) count[b] = 0;
-    const int lane = threadIdx.x & 63;
-    const int nwaves = gridDim.x * (blockDim.x / 64);
-    const int nfb = *fb_count;
-    for (int f = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); f < nfb; f += nwaves) {
-        const int p = fb_list[f];
-        const double x = qx[p], y = qy[(long)p * ys], z = qz[(long)p * zs];
-        double bd = kSentinel;
-        int bx = INT_MAX;
-        int j = lane;
-        for (; j + 64 < ncells; j += 128) {  // two cells per round
-            const double ax = cells[j], ay = cells[stride + j], az = cells[2 * stride + j];
-            const double cx = cells[j + 64], cy = cells[stride + j + 64], cz = cells[2 * stride + j + 64];
-            take(dist2_q(ax, ay, az, x, y, z), j, bd, bx);
-            take(dist2_q(cx, cy, cz, x, y, z), j + 64, bd, bx);
-        }
-        if (j < ncells) take(dist2_q(cells[j], cells[stride + j], cells[2 * stride + j], x, y, z), j, bd, bx);
-        const unsigned long long kd = wave_min_u64((unsigned long long)__double_as_longlong(bd));
-        const bool at = (unsigned long long)__double_as_longlong(bd) == kd;
-        const unsigned long long ki = wave_min_u64(at ? (unsigned long long)(unsigned)bx : ~0ull);
-        if (lane == 0) {
-            const double d = __longlong_as_double((long long)kd);
-            const int i = (d < kSentinel && ki != ~0ull) ? (int)ki : -1;
-            best_i[p] = i;
-            if (best_d) best_d[p] = d;
-            if (zeta0) zeta0[p] = i >= 0 ? cells[3 * stride + i] : 0.0;  // MCsub.jl:249
-        }
+    if (!proven) {  // rare: every cell, the same half-wave (index order inside each lane)
+        bd = kSentinel;
+        bx = INT_MAX;
+        for (int j = hl; j < ncells; j += 32)
+            take(dist2_q(cells[j], cells[stride + j], cells[2 * (long)stride + j], x, y, z), j, bd, bx);
+        half_min(bd, bx);
+    }
+    if (hl == 0 && p < npts) {
+        const bool found = bd < kSentinel;
+        best_i[p] = found ? bx : -1;
+        if (best_d) best_d[p] = bd;
+        if (zeta0) zeta0[p] = found ? zeta_cells[bx] : 0.0;  // MCsub.jl:249
     }
 }
 
 }  // namespace
 
 hipError_t launch_nearest_grid(const double *qx, const double *qy, const double *qz, int64_t npts,
-                               int64_t qy_stride, int64_t qz_stride, const double *cells, int64_t stride,
+                               int64_t qy_stride, int64_t qz_stride, double *cells, int64_t stride,
                                int64_t ncells, const CellGrid &G, NNWork &work, int num_cus, int *best_i,
-                               double *best_d, double *zeta0, hipStream_t s, Timer *tm) {
+                               double *best_d, double *zeta0, hipStream_t s, Timer *tm, const double *stage) {
     if (npts <= 0) return hipSuccess;
     const int64_t nb = (int64_t)G.gx * G.gy * G.gz;
     if (nb > kGridMaxBuckets || ncells <= 0) return hipErrorInvalidValue;
@@ -187,29 +175,33 @@ hipError_t launch_nearest_grid(const double *qx, const double *qy, const double 
         if (e == hipSuccess) cap = need;
     };
     const size_t had = work.g_count_cap;
-    grow(reinterpret_cast<void *&>(work.g_count), work.g_count_cap, sizeof(int) * (size_t)nb);
-    if (e == hipSuccess && work.g_count_cap != had)  // fresh counters start at zero; later ones are
-        e = hipMemsetAsync(work.g_count, 0, work.g_count_cap, s);  // left zero by k_nn_fallback
+    grow(reinterpret_cast<void *&>(work.g_count), work.g_count_cap, 2 * sizeof(int) * (size_t)nb);
+    if (e == hipSuccess && work.g_count_cap != had) {  // fresh counters start at zero; later ones are
+        e = hipMemsetAsync(work.g_count, 0, work.g_count_cap, s);  // zeroed by the alternate search
+        work.g_par = 0;
+        work.g_used[0] = work.g_used[1] = 0;
+    }
     grow(reinterpret_cast<void *&>(work.g_ent), work.g_ent_cap, sizeof(BucketEntry) * (size_t)nb * kGridCap);
-    grow(reinterpret_cast<void *&>(work.g_fb), work.g_fb_cap, sizeof(int) * (size_t)(npts + 1));
     if (e != hipSuccess) return e;
-    int *fb_count = work.g_fb + npts;
+    const int64_t half = (int64_t)(work.g_count_cap / (2 * sizeof(int)));
+    const int par = work.g_par;
+    int *count = work.g_count + par * half, *other = work.g_count + (par ^ 1) * half;
     hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
-    hipLaunchKernelGGL(k_grid_fill, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, s, cells, (int)stride,
-                       (int)ncells, G, work.g_count, work.g_ent, fb_count);
+    hipLaunchKernelGGL(k_grid_fill, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, s, cells, stage,
+                       (int)stride, (int)ncells, G, count, work.g_ent);
     if (tm) tm->end("nn_grid_build", t0, s);
     hipEvent_t t1 = tm ? tm->begin(s) : nullptr;
     hipLaunchKernelGGL(k_nn_grid, dim3((unsigned)((npts + 7) / 8)), dim3(256), 0, s, qx, qy, qz, (int)npts,
-                       (int)qy_stride, (int)qz_stride, G, work.g_count, work.g_ent, cells + 3 * stride, best_i,
-                       best_d, zeta0, work.g_fb, fb_count);
+                       (int)qy_stride, (int)qz_stride, G, count, work.g_ent, cells, (int)stride, (int)ncells,
+                       best_i, best_d, zeta0, other, (int)work.g_used[par ^ 1]);
     if (tm) tm->end("nn_grid", t1, s);
-    hipEvent_t t2 = tm ? tm->begin(s) : nullptr;
-    const int blocks = std::max(1, std::min<int>(num_cus * 2, (int)((npts + 3) / 4)));
-    hipLaunchKernelGGL(k_nn_fallback, dim3(blocks), dim3(256), 0, s, qx, qy, qz, (int)qy_stride, (int)qz_stride,
-                       work.g_fb, fb_count, cells, (int)stride, (int)ncells, best_i, best_d, zeta0, work.g_count,
-                       (int)nb);
-    if (tm) tm->end("nn_fallback", t2, s);
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        work.g_used[par ^ 1] = 0;
+        work.g_used[par] = nb;
+        work.g_par = par ^ 1;
+    }
+    return e;
 }
 
 }  // namespace tdstar
