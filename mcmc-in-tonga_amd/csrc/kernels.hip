@@ -163,15 +163,15 @@ __global__ __launch_bounds__(256) void k_ray_sums(const int *__restrict__ ray_of
 }
 
 // ---------------------------------------------------------------------------
-// Stage 3: chi^2, MCsub.jl:169-172, strictly sequential in k, fused into the
-// ray-sum launch: the last workgroup to finish its rays (a device-scope
-// counter) computes the terms and reproduces the k-order sum exactly with
-// binade-segmented integer scans (exact_sum.h) -- the whole workgroup for long
-// sums, one wave for short ones and whenever the workgroup's guess fails.
+// Stage 3: chi^2, MCsub.jl:169-172, strictly sequential in k, reproduced
+// exactly with binade-segmented integer scans (exact_sum.h).  Up to kChi2Lds
+// rays it is fused into the ray-sum launch: the last workgroup to finish its
+// rays (a device-scope counter) stages the terms in LDS and one wave sums
+// them.  Longer ray lists get a 1024-thread launch of their own (k_chi2): the
+// block-wide scan, the one-wave sum if its guess fails.
 // ---------------------------------------------------------------------------
-constexpr int kChi2Threads = 1024;    // the exact-sum test kernel
-constexpr int kExactMinTerms = 2048;  // below: the one-wave sum is as fast
-constexpr int kChi2Lds = 2048;        // terms staged in LDS up to this many rays
+constexpr int kChi2Threads = 1024;
+constexpr int kChi2Lds = 2048;  // fused up to this many rays
 
 __global__ __launch_bounds__(256) void k_ray_sums_chi2(const int *__restrict__ ray_off, int n,
                                                        const double *__restrict__ w,
@@ -182,7 +182,6 @@ __global__ __launch_bounds__(256) void k_ray_sums_chi2(const int *__restrict__ r
                                                        double *host_out) {
     __shared__ double scratch[4][96];
     __shared__ double lterm[kChi2Lds];
-    __shared__ ExactSumLds xs;
     __shared__ int last;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ray = blockIdx.x * 4 + wv;
@@ -195,31 +194,53 @@ __global__ __launch_bounds__(256) void k_ray_sums_chi2(const int *__restrict__ r
             if (host_out) host_out[1 + ray] = r;  // pinned host memory: [phi, ptS]
         }
     }
+    if (n > kChi2Lds) return;  // long ray lists: k_chi2 (a launch of its own) follows
     __threadfence();  // this workgroup's ptS, device-wide, before it counts itself done
     __syncthreads();
     if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
     __threadfence();  // every other workgroup's ptS
-    const bool lds = n <= kChi2Lds;
-    double *t = lds ? lterm : terms;
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
         const double d = ptS[k] - tS[k];
         const double sg = sig[k];
-        t[k] = ((d * d) * 1.0) / (sg * sg);  // MCsub.jl:171
+        lterm[k] = ((d * d) * 1.0) / (sg * sg);  // MCsub.jl:171
     }
     __syncthreads();
     double C = 0.0;
-    bool ok = false;
-    if (n >= kExactMinTerms) ok = block_exact_sum<256>(t, n, 0.0, nullptr, &C, xs);
-    if (!ok && wv == 0) {
+    if (wv == 0) {
         bool stopped = false;
-        C = wave_seq_sum(t, n, 0.0, nullptr, lane, nullptr, &stopped);
+        C = wave_seq_sum(lterm, n, 0.0, nullptr, lane, nullptr, &stopped);
     }
     if (threadIdx.x == 0) {
         *phi = C;
         if (host_out) host_out[0] = C;
         *done = 0u;  // ready for the next evaluation
+        __threadfence_system();
+    }
+}
+
+__global__ __launch_bounds__(kChi2Threads) void k_chi2(const double *__restrict__ ptS,
+                                                       const double *__restrict__ tS,
+                                                       const double *__restrict__ sig, int n,
+                                                       double *__restrict__ terms, double *__restrict__ phi,
+                                                       double *host_out) {
+    __shared__ ExactSumLds w;
+    for (int k = threadIdx.x; k < n; k += kChi2Threads) {
+        const double d = ptS[k] - tS[k];
+        const double s = sig[k];
+        terms[k] = ((d * d) * 1.0) / (s * s);  // MCsub.jl:171
+    }
+    __syncthreads();
+    double C = 0.0;
+    const bool done = block_exact_sum<kChi2Threads>(terms, n, 0.0, nullptr, &C, w);
+    if (!done && threadIdx.x < 64) {
+        bool stopped = false;
+        C = wave_seq_sum(terms, n, 0.0, nullptr, (int)threadIdx.x, nullptr, &stopped);
+    }
+    if (threadIdx.x == 0) {
+        *phi = C;
+        if (host_out) host_out[0] = C;
         __threadfence_system();
     }
 }
@@ -340,6 +361,9 @@ hipError_t launch_ray_sums_chi2(const Geometry &g, const double *zeta0, double *
     hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
     hipLaunchKernelGGL(k_ray_sums_chi2, dim3((unsigned)((g.n + 3) / 4)), dim3(256), 0, s, g.ray_off, (int)g.n, g.w,
                        zeta0, ptS, g.tS, g.sig, g.terms, phi, g.done, host_out);
+    if (g.n > kChi2Lds)
+        hipLaunchKernelGGL(k_chi2, dim3(1), dim3(kChi2Threads), 0, s, ptS, g.tS, g.sig, (int)g.n, g.terms, phi,
+                           host_out);
     if (tm) tm->end("ray_sums_chi2", t0, s);
     return hipGetLastError();
 }
