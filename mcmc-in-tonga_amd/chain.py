@@ -195,3 +195,23 @@ def _save_checkpoint(d, chain, it, n_iter, model, hist, seed):
     for f in glob.glob(os.path.join(d, "chain%d_iter*.npz" % chain)):  # keep the newest only (:53-55)
         if f != path:
             os.remove(f)
+
+
+def main_inversion(TD_parameters=None, dataStruct=None, out="model.jld", checkpoint_dir=None,  # noqa: N803
+                   engine=_lib.TD_ENGINE_DEVICE):
+    """main_inversion.jl:11-18: the chains (one after another on this GPU; one
+    rank per GPU for more, see tempering/bench), the posterior maps of
+    plot_model_hist (numbers only) and ``save(out, "model", models)`` in JLD.
+    Returns (models, maps)."""
+    from . import jld
+    from .config import define_TDstructrure
+    from .data import load_data_Tonga
+    from .posterior import plot_model_hist
+    TD_parameters = TD_parameters or define_TDstructrure()
+    dataStruct = dataStruct or load_data_Tonga(TD_parameters)
+    models = [TD_inversion_function(TD_parameters, dataStruct, c, engine=engine, checkpoint_dir=checkpoint_dir)
+              for c in range(1, int(TD_parameters.n_chains) + 1)]
+    maps = plot_model_hist(models, dataStruct, TD_parameters, 20.0)
+    if out:
+        jld.save(out, models)
+    return models, maps

@@ -19,9 +19,13 @@ plain ``.npz`` (numpy, ``allow_pickle=False``-loadable) and are committed:
   ``Data/ak135f.txt`` (used to synthesise slowness U).
 * ``tests/golden/model_jld_kat.npz`` -- the known-answer records of
   ``model.jld`` (2 chains x 50 saved ``Model`` structs, DefStruct.jl:32-48):
-  cells, zeta, phi, ptS, tS, likelihood.  These pin the chi^2 reduction
+  cells, zeta, phi, ptS, tS, likelihood, action, accept, zeta_xz, zeta_xy,
+  and same_as (the saved position whose object a position aliases).  These pin the chi^2 reduction
   (MCsub.jl:169-173) and the likelihood expression (MCsub.jl:179-182), whose
   value also pins Julia's reassociated ``sum`` order (see oracle/README).
+* ``tests/golden/model_jld_structure.json`` -- the HDF5 structure of
+  ``model.jld`` (user block, objects, storage layouts, types, attributes):
+  the JLD writer (mcmc-in-tonga_amd/jld_h5.py) must reproduce it.
 """
 import os
 import sys
@@ -86,18 +90,23 @@ def model_kat():
     dt = np.dtype([(n, (h5py.ref_dtype if t == "R" else t)) for n, t in zip(MODEL_FIELDS, MODEL_FMT)])
     mt = h5py.h5t.py_create(dt)
     recs = []
+    first = {}  # a Model saved twice (model_hist aliasing) is one stored object
     top = f["model"]
     for c in range(top.shape[0]):
         chain = f[top[c]]
         for j in range(chain.shape[0]):
             d = f[chain[j]]
+            addr = h5py.h5o.get_info(d.id).addr
+            first.setdefault(addr, len(recs))
             a = np.empty((), dtype=dt)
             d.id.read(h5py.h5s.ALL, h5py.h5s.ALL, a, mtype=mt)
             g = lambda k: np.asarray(f[a[k][()]][()], dtype=np.float64)
             recs.append(dict(chain=c + 1, nCells=float(a["nCells_"]), x=g("xCell_"), y=g("yCell_"),
                              z=g("zCell_"), zeta=g("zeta_"), phi=float(a["phi_"]), ptS=g("ptS_"),
                              tS=g("tS_"), likelihood=float(a["likelihood_"]),
-                             action=int(a["action_"]), accept=int(a["accept_"])))
+                             action=int(a["action_"]), accept=int(a["accept_"]),
+                             zeta_xz=float(a["zeta_xz_"]), zeta_xy=float(a["zeta_xy_"]),
+                             same_as=first[addr]))
     tS = recs[0]["tS"]
     assert all((r["tS"] == tS).all() for r in recs)
     ncell = np.array([len(r["x"]) for r in recs], dtype=np.int64)
@@ -115,10 +124,25 @@ def model_kat():
         likelihood=np.array([r["likelihood"] for r in recs]),
         action=np.array([r["action"] for r in recs], dtype=np.int64),
         accept=np.array([r["accept"] for r in recs], dtype=np.int64),
+        zeta_xz=np.array([r["zeta_xz"] for r in recs]),
+        zeta_xy=np.array([r["zeta_xy"] for r in recs]),
+        same_as=np.array([r["same_as"] for r in recs], dtype=np.int64),
         ptS=np.stack([r["ptS"] for r in recs]),
         tS=tS,
     )
     print("model.jld: %d models, %d data" % (len(recs), len(tS)))
+
+
+def model_jld_structure():
+    """The HDF5 structure of model.jld (jld_h5.fingerprint): what the JLD
+    writer must reproduce for the same models (tests/test_jld.py)."""
+    import json
+    sys.path.insert(0, os.path.join(REPO, "mcmc-in-tonga_amd"))
+    import jld_h5
+    fp = jld_h5.fingerprint(os.path.join(REF, "model.jld"))
+    with open(os.path.join(HERE, "model_jld_structure.json"), "w") as fh:
+        json.dump(fp, fh)
+    print("model.jld structure: %d entries" % len(fp))
 
 
 if __name__ == "__main__":
@@ -128,3 +152,4 @@ if __name__ == "__main__":
     rays()
     ak135()
     model_kat()
+    model_jld_structure()
