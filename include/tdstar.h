@@ -123,6 +123,17 @@ int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const 
                    int64_t ny, const double *Z, int64_t nz, double *zeta_out, int32_t *nearest_out,
                    int64_t *npoints_out);
 
+/* Slowness of ray points from a gridded 3-D model: pre_process_data.jl:34
+ * `itp.(ix, iy, iz)` with load_3Dvel.jl:32 `interpolate((x, y, z), sn,
+ * Gridded(Linear()))`.  Knots strictly increasing (>= 2 per
+ * axis); values column-major nx x ny x nz (x fastest, Julia's sn[1,:,:,:]).
+ * A point outside the grid (Interpolations.jl: BoundsError) gets NaN and is
+ * counted in *n_outside.  Context-free (no ray geometry needed): runs on
+ * `device`, synchronous.  td_last_error(NULL) on failure. */
+int td_trilinear(int device, const double *xs, int64_t nx, const double *ys, int64_t ny, const double *zs,
+                 int64_t nz, const double *values, const double *px, const double *py, const double *pz,
+                 int64_t npts, double *out, int64_t *n_outside);
+
 /* ------------------------------------------------------------------------
  * Posterior maps -- the numbers of plot_model_hist (MCsub.jl:753-825), not the
  * plots.  For nq query points (a cross-section: MCsub.jl:765-768 xz at y =

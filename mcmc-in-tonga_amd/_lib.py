@@ -59,6 +59,8 @@ SIGNATURES = {
     "td_evaluate_batch": (ctypes.c_int, [_vp, _i64, _pi64, _pd, _pd, _pd, _pd, _pd, _pd, _pd]),
     "td_interpolate": (ctypes.c_int, [_vp, _pd, _pd, _pd, _pd, _i64, _pd, _i64, _pd, _i64, _pd, _i64, _pd, _pi32,
                                       _pi64]),
+    "td_trilinear": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _pd, _i64, _pd, _i64, _pd, _pd, _pd, _pd, _i64, _pd,
+                                     _pi64]),
     "td_rasterize": (ctypes.c_int, [_vp, _i64, _pi64, _pd, _pd, _pd, _pd, _pd, _pd, _pd, _i64, _pd, _pd, _pd]),
     "td_chain_create": (ctypes.c_int, [ctypes.POINTER(_vp), _vp, ctypes.POINTER(TdChainParams), _pd, _pd, _pd, _pd,
                                        _i64]),

@@ -96,14 +96,19 @@ def pad_rays(npts, px, py, pz, m=None):
 
 
 def _datastruct(rayX, rayY, rayZ, tS, allSig, extra=None):
-    U = ak135_slowness(rayZ)
+    return _datastruct_u(rayX, rayY, rayZ, ak135_slowness(rayZ), tS, allSig, extra)
+
+
+def _datastruct_u(rayX, rayY, rayZ, U, tS, allSig, extra=None):
+    """DataStruct from rays and their slowness (load_data_Tonga.jl:66-88)."""
     rayL, rayU = segments(rayX, rayY, rayZ, U)
     e = extra or {}
     nan = np.full(len(tS), np.nan)
     return DataStruct(
         tS=np.asarray(tS, dtype=np.float64), allaveatten=e.get("allaveatten", nan), allLats=e.get("allLats", nan),
         allLons=e.get("allLons", nan), allSig=np.asarray(allSig, dtype=np.float64), dataX=e.get("dataX", nan),
-        dataY=e.get("dataY", nan), xVec=julia_range(*XVEC), yVec=julia_range(*YVEC), zVec=julia_range(*ZVEC),
+        dataY=e.get("dataY", nan), xVec=e.get("xVec", julia_range(*XVEC)), yVec=e.get("yVec", julia_range(*YVEC)),
+        zVec=e.get("zVec", julia_range(*ZVEC)),
         elonsX=e.get("elonsX", nan), elatsY=e.get("elatsY", nan), elons=e.get("elons", nan),
         elats=e.get("elats", nan), edep=e.get("edep", nan), coastX=np.zeros(0), coastY=np.zeros(0),
         rayX=rayX, rayY=rayY, rayZ=rayZ, rayL=rayL, rayU=rayU, U=U)

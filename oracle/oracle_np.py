@@ -151,3 +151,33 @@ def rasterize(models, qx, qy, qz):
     with np.errstate(invalid="ignore", divide="ignore"):
         std = np.sqrt(julia_mapreduce_arrays(dev) / float(n - 1))
     return mean, std, np.array(vals)
+
+
+def trilinear(xs, ys, zs, values, px, py, pz):
+    """Gridded(Linear()) of Interpolations.jl as used at load_3Dvel.jl:32 and
+    pre_process_data.jl:34 (restated: the package is not in the reference tree
+    and its version is unpinned -- the 8-corner association below is this
+    build's, shared with ingest.hip; parity unpinned for the last ulps).
+    Per axis: i = searchsortedlast(knots, x) clamped to [1, n-1] (0-based
+    [0, n-2]), t = (x - k_i) / (k_{i+1} - k_i); outside [k_1, k_n] -> NaN (the
+    reference throws a BoundsError).  values[i, j, k]; lerp x, then y, then z."""
+    xs, ys, zs = (np.asarray(a, dtype=np.float64) for a in (xs, ys, zs))
+    v = np.asarray(values, dtype=np.float64)
+    px, py, pz = (np.asarray(a, dtype=np.float64).ravel() for a in (px, py, pz))
+
+    def axis(k, x):
+        i = np.clip(np.searchsorted(k, x, side="right") - 1, 0, len(k) - 2)
+        ok = (x >= k[0]) & (x <= k[-1])
+        t = (x - k[i]) / (k[i + 1] - k[i])
+        return i, t, ok
+
+    i, tx, okx = axis(xs, px)
+    j, ty, oky = axis(ys, py)
+    k, tz, okz = axis(zs, pz)
+    ux, uy, uz = 1.0 - tx, 1.0 - ty, 1.0 - tz
+    c2 = []
+    for dz in (0, 1):
+        c1 = [ux * v[i, j + dy, k + dz] + tx * v[i + 1, j + dy, k + dz] for dy in (0, 1)]
+        c2.append(uy * c1[0] + ty * c1[1])
+    out = uz * c2[0] + tz * c2[1]
+    return np.where(okx & oky & okz, out, np.nan)
