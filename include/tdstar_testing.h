@@ -34,9 +34,10 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
  * accept, commit), [8..11] whole proposals by action (birth, death, change,
  * move), [12..13] commit / next proposal, [14] proven early rejections, [15]
  * grid searches that fell back to a full scan, [16 + 10 (action-1) + j] the
- * phases split by action (j: A..F, commit, next proposal, final barrier).
+ * phases split by action (j: A..F, commit, next proposal, final barrier),
+ * [56 + w] phase F of wave w, [64] chi^2 tail terms, [65] chi^2 scan rounds.
  * Never enabled in measured runs. */
-int tdt_chain_profile(td_chain *ch, int enable, int64_t out[64]);
+int tdt_chain_profile(td_chain *ch, int enable, int64_t out[72]);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);

@@ -67,6 +67,7 @@ tdchain::Params make_params(const td_chain_params &p) {
     const double two_pi_sqrt = 2.5066282746310002;
     P.log_prior_birth = std::log((P.sig_zeta * two_pi_sqrt) / P.zeta_scale);
     P.log_prior_death = std::log(P.zeta_scale / (P.sig_zeta * two_pi_sqrt));
+    tdchain::params_derived(P);
     return P;
 }
 
@@ -544,7 +545,8 @@ int td_chain_set_temperature(td_chain *ch, double temperature) {
     if (!ch || !(temperature > 0.0)) return chain_err(ch, TD_ERR_ARG, "td_chain_set_temperature: need T > 0");
     ch->prm.temperature = temperature;
     ch->P.temperature = temperature;
-    ch->dev.params.temperature = temperature;
+    tdchain::params_derived(ch->P);
+    ch->dev.params = ch->P;
     return TD_OK;
 }
 
@@ -582,7 +584,7 @@ int tdt_chain_set_lds_mode(td_chain *ch, int mode) {
     return TD_OK;
 }
 
-int tdt_chain_profile(td_chain *ch, int enable, int64_t out[64]) {
+int tdt_chain_profile(td_chain *ch, int enable, int64_t out[72]) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE) return TD_ERR_ARG;
     ch->dev.profile = enable;
     if (out) {

@@ -26,7 +26,7 @@
 namespace tdstar {
 
 constexpr int kTilePts = 16;
-constexpr int kProfSlots = 64;
+constexpr int kProfSlots = 72;
 constexpr int kChainThreads = 512;  // 8 waves: 256 VGPRs per lane, no spills
 constexpr int kBucketCap = 32;
 
@@ -38,7 +38,8 @@ struct ChainScalars {
     double phi;
     int64_t bytes;         // algorithmic global-memory bytes the proposals needed (roofline)
     int64_t prof[kProfSlots];  // diagnostic (DevChain::profile): cycles per phase [0..13], [14] proven
-                               // rejections, [15] grid fallbacks, [16 + 10 (action-1) + j] per-action phases
+                               // rejections, [15] grid fallbacks, [16 + 10 (action-1) + j] per-action phases,
+                               // [56 + wave] phase F per wave, [64] chi^2 tail terms, [65] chi^2 scan rounds
     int ncells;            // cells in the model
     int nslots;            // slot high-water mark
     int nfree;             // free-slot stack depth

@@ -726,10 +726,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     double C = big ? C_big : (k0 > 0 ? v.prefix[k0 - 1] : 0.0);  // MCsub.jl:169 C = 0
                     if (!big && k0 < n) {
                         bool stopped = false;
-                        C = wave_seq_sum(v.term + k0, n - k0, C, v.cprefix + k0, lane, &sh.early_reject, &stopped);
+                        C = wave_seq_sum(v.term + k0, n - k0, C, v.cprefix + k0, lane, &sh.early_reject, &stopped,
+                                         prof_on ? &sh.prof[65] : nullptr);
+                        if (prof_on && lane == 0) sh.prof[64] += n - k0;
                     }
                     phi_n = k0 < n ? C : sh.phi;
                 }
+                if (prof_on && lane == 0) sh.prof[66] += clock64() - tF;  // diagnostic: scan done
             }
             if (tid == 0) {
                 const int k0 = sh.k0;
@@ -741,6 +744,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 acc_r = acc;
                 sh.accept = acc ? 1 : 0;
                 sh.phi_n = phi_n;
+                if (prof_on) sh.prof[67] += clock64() - tF;  // diagnostic: decision taken
                 if (acc) {
                     sh.g_op = action == tdchain::kBirth ? 2 : action == tdchain::kDeath ? 1
                               : action == tdchain::kMove ? 3 : 0;
@@ -753,19 +757,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.g_nz = pp.z;
                     atomicAdd((unsigned long long *)&sh.accepted[action], 1ull);
                 }
-                // accounting, off the decision's path (no-return LDS atomics)
                 if (prof_on && early) atomicAdd((unsigned long long *)&sh.prof[14], 1ull);  // proven rejections
-                if (fwd) {
-                    atomicAdd((unsigned long long *)&sh.evaluations, 1ull);
-                    // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
-                    // candidate points (coords + cached slot/distance, 36 B), grid queries
-                    // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
-                    // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
-                    atomicAdd((unsigned long long *)&sh.bytes,
-                              (unsigned long long)((long long)NT * 32 + (long long)sh.pts_seen * 36 +
-                                                   (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
-                                                   (long long)sh.ray_pts * 17 + (long long)(n - k0) * 28));
-                }
             } else if (tid == 64) {  // the next proposal as if this one were rejected
                 if (can_spec) {
                     make_proposal(sh.ps[sh.cur ^ 1], P, draws[(it + 1) & 63], ncells, sh.nfree, sh.nslots, d.free_slots, d.cx,
@@ -777,6 +769,17 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     grid_prefetch(d, sh, lane, action, action == tdchain::kBirth ? new_slot : slot_k, kx, ky,
                                   kz, pp.x, pp.y, pp.z);
             } else if (wv == kWaves - 2) {
+                if (lane == 0 && fwd) {  // accounting, off wave 0's path
+                    atomicAdd((unsigned long long *)&sh.evaluations, 1ull);
+                    // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
+                    // candidate points (coords + cached slot/distance, 36 B), grid queries
+                    // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
+                    // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
+                    atomicAdd((unsigned long long *)&sh.bytes,
+                              (unsigned long long)((long long)NT * 32 + (long long)sh.pts_seen * 36 +
+                                                   (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
+                                                   (long long)sh.ray_pts * 17 + (long long)(n - sh.k0) * 28));
+                }
                 if (lane == 0 && (action == tdchain::kBirth || action == tdchain::kDeath)) {
                     sh.lnN_far[0] = d.logN[max(ncells - 2, 0)];
                     sh.lnN_far[1] = d.logN[ncells + 2];

@@ -215,9 +215,17 @@ struct Params {
     double xr, yr, zr;                     // (sig/100)*(max-min), :30-32
     double temperature;
     // log of the constant prior factors of the birth / death ratios (:96-97,
-    // :151-152), for reject_bound only (host libm; the bound has a wide margin)
+    // :151-152), and 1/(2T), 1/(2 sig_zeta^2): computed once on the host (libm),
+    // the same numbers in both engines
     double log_prior_birth, log_prior_death;
+    double inv_2t, inv_2sig2;
 };
+
+// the derived constants of Params (after any change of temperature or sig_zeta)
+inline void params_derived(Params &P) {
+    P.inv_2t = 1.0 / (2.0 * P.temperature);
+    P.inv_2sig2 = 1.0 / (2.0 * P.sig_zeta * P.sig_zeta);
+}
 
 // What the iteration proposes, before any forward-model evaluation.
 struct Proposal {
@@ -308,14 +316,15 @@ inline void log_window(double out[3], int64_t N) {
 // register; tools/repro_accept.hip).
 TD_HD double log_alpha(const Params &P, const Proposal &p, double phi, double phi_n, double czeta,
                        double zeta_killed, double zetanew_death, const double *lnN) {
-    const double g = (phi - phi_n) / (2.0 * P.temperature);  // change eq. 15 (:196), move eq. 14 (:241)
+    // (multiplications by precomputed 1/(2T), 1/(2 sig^2): no division on the device's decision path)
+    const double g = (phi - phi_n) * P.inv_2t;  // change eq. 15 (:196), move eq. 14 (:241)
     double la = g;
     if (p.action == kBirth) {  // eq. 16, :96-97: (N/(N+1)) (sig_zeta sqrt(2 pi) / zeta_scale) exp(dz^2/(2 sig^2) - dphi)
         const double dz = czeta - p.zeta;
-        la = ((lnN[1] - lnN[2]) + P.log_prior_birth) + ((dz * dz) / (2.0 * P.sig_zeta * P.sig_zeta) + g);
+        la = ((lnN[1] - lnN[2]) + P.log_prior_birth) + ((dz * dz) * P.inv_2sig2 + g);
     } else if (p.action == kDeath) {  // eq. 17, :151-152: (N/(N-1)) (zeta_scale / (sig_zeta sqrt(2 pi))) exp(-dz^2/(2 sig^2) - dphi)
         const double dz = zeta_killed - zetanew_death;
-        la = ((lnN[1] - lnN[0]) + P.log_prior_death) + (g - (dz * dz) / (2.0 * P.sig_zeta * P.sig_zeta));
+        la = ((lnN[1] - lnN[0]) + P.log_prior_death) + (g - (dz * dz) * P.inv_2sig2);
     }
     return la;
 }
@@ -335,7 +344,7 @@ TD_HD double reject_bound(const Params &P, const Proposal &p, double phi, double
                           double zetanew_death, const double *lnN) {
     if (!(p.u_accept > 0.0)) return __builtin_huge_val();
     const double lf = log_alpha(P, p, phi, phi, czeta, zeta_killed, zetanew_death, lnN);  // dphi = 0
-    return phi + 2.0 * P.temperature * (lf - p.log_u);
+    return phi + 2.0 * P.temperature * (lf - p.log_u);  // (a bound: its own rounding is covered by the margin)
 }
 
 }  // namespace tdchain

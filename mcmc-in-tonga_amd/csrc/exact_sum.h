@@ -343,11 +343,12 @@ __device__ __forceinline__ double p2(int biased) {  // 2^(biased - 1023), 1 <= b
 }  // namespace wseq
 
 __device__ __forceinline__ double wave_seq_sum(const double *t, int cnt, double C, double *out, int lane,
-                                               const int *stop, bool *stopped) {
+                                               const int *stop, bool *stopped, long long *rounds = nullptr) {
     using namespace wseq;
     int pos = 0;
     double tv = lane < cnt ? t[lane] : 0.0;  // the window [pos, pos + 64)
     while (pos < cnt) {
+        if (rounds && lane == 0) *rounds += 1;  // diagnostic
         const int lim = min(64, cnt - pos);
         // the next window, if this round keeps all 64 terms
         const double tn = pos + 64 + lane < cnt ? t[pos + 64 + lane] : 0.0;

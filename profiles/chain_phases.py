@@ -31,13 +31,13 @@ def main():
     ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000, chain=1), tt.random_model(N, 3))
     ch.run(2000)
     L = tt.lib()
-    out0 = (ctypes.c_int64 * 64)()
+    out0 = (ctypes.c_int64 * 72)()
     L.tdt_chain_profile(ch.h, 1, out0)
     st0 = ch.stats()
     t0 = time.perf_counter()
     ch.run(iters)
     el = time.perf_counter() - t0
-    out = (ctypes.c_int64 * 64)()
+    out = (ctypes.c_int64 * 72)()
     L.tdt_chain_profile(ch.h, 0, out)
     cyc = np.array(out[:7], dtype=np.float64) - np.array(out0[:7], dtype=np.float64)
     cyc[6] += (out[12] - out0[12]) + (out[13] - out0[13])  # G = commit + next proposal + barrier
@@ -65,6 +65,11 @@ def main():
         for i, a in enumerate(["birth", "death", "change", "move"])}
     res["F per wave (cycles per iter): chi2 scan, next proposal, tile maxima x4, bound, grid prefetch"] = [
         round((out[56 + w] - out0[56 + w]) / iters, 1) for w in range(8)]
+    ev = max(sum(prop), 1)
+    res["chi2 tail terms per proposal"] = round((out[64] - out0[64]) / ev, 1)
+    res["chi2 scan rounds per proposal"] = round((out[65] - out0[65]) / ev, 2)
+    res["F wave 0: cycles to scan end / to decision (per iter)"] = [round((out[66] - out0[66]) / iters, 1),
+                                                                     round((out[67] - out0[67]) / iters, 1)]
     print(json.dumps(res, indent=1))
 
 
