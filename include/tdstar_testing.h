@@ -55,6 +55,12 @@ int tdt_exact_sum(int device, const double *term, int64_t cnt, double C0, double
 /* The one-wave exact sequential sum (exact_sum.h wave_seq_sum, the chain's
  * chi^2 tail): same contract as tdt_exact_sum, always exact; *fallbacks =
  * 256-term chunks that needed the slower binade-by-binade path.  Needs a GPU. */
+/* The one-wave sum after a few terms changed (exact_sum.h wave_delta_sum, the
+ * chain's chi^2): prefix[k] = C0 + term[0] + ... + term[k] left to right,
+ * given old_prefix (the same sums over the old terms) and changed[k] != 0
+ * where term[k] differs from the old term.  Needs a GPU. */
+int tdt_wave_delta_sum(int device, const double *term, const double *old_prefix, const int *changed, int64_t cnt,
+                       double C0, double *prefix, double *C_end);
 int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, double *prefix, double *C_end,
                      int *fallbacks);
 

@@ -513,6 +513,26 @@ int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, dou
     return e == hipSuccess ? TD_OK : TD_ERR_HIP;
 }
 
+int tdt_wave_delta_sum(int device, const double *term, const double *old_prefix, const int *changed, int64_t cnt,
+                       double C0, double *prefix, double *C_end) {
+    if (!term || !old_prefix || !changed || !prefix || !C_end || cnt < 1 || cnt > (1 << 24)) return TD_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return TD_ERR_HIP;
+    const size_t nb = sizeof(double) * (size_t)cnt;
+    void *buf = nullptr;
+    if (hipMalloc(&buf, 3 * nb + sizeof(double) + sizeof(int) * (size_t)cnt) != hipSuccess) return TD_ERR_NOMEM;
+    double *dt = static_cast<double *>(buf), *dold = dt + cnt, *dp = dold + cnt, *de = dp + cnt;
+    int *dc = reinterpret_cast<int *>(de + 1);
+    hipError_t e = hipMemcpy(dt, term, nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dold, old_prefix, nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dc, changed, sizeof(int) * (size_t)cnt, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = test_wave_delta_sum(dt, dold, dc, (int)cnt, C0, dp, de);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(prefix, dp, nb, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(C_end, de, sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(buf);
+    return e == hipSuccess ? TD_OK : TD_ERR_HIP;
+}
+
 int tdt_set_nn_method(td_ctx *ctx, int method) {
     if (!ctx || method < 0 || method > 2) return TD_ERR_ARG;
     ctx->nn_method = method;

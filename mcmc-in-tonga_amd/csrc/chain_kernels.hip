@@ -46,7 +46,6 @@ using tdchain::Proposal;
 constexpr int kWaves = kChainThreads / 64;
 static_assert(kTilePts == 16, "a tile is one 16-lane DPP row (row_max_u64)");
 constexpr int kOrphanLds = 256; // orphan records kept in LDS (more: read back from HBM)
-constexpr int kChainExactMin = 1024;  // chi^2 tails from this length on: block-wide exact scan
 
 // A point whose nearest cell is removed or moved: re-searched in phase D.
 struct OrphanRec {
@@ -155,7 +154,7 @@ struct Shared {
 
 // LDS carve-up (host and device agree on it through this function).
 struct LdsPlan {
-    size_t scratch, draws, exact, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
+    size_t scratch, draws, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
         tS, sig, rflag, rhit, ord, total;
 };
 
@@ -166,9 +165,6 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
     size_t o = align16(sizeof(Shared));
     L.scratch = o; o += align16(sizeof(double) * kWaves * 96);
     L.draws = o; o += align16(sizeof(tdchain::Draws) * 64);                     // 64 iterations ahead
-    if (!small) {  // long chi^2 tails: the block-wide exact scan (exact_sum.h)
-        L.exact = o; o += align16(sizeof(ExactSumLds));
-    }
     if (small) {
         L.tlo = o; o += align16(sizeof(float) * 3 * ntiles);
         L.thi = o; o += align16(sizeof(float) * 3 * ntiles);
@@ -702,18 +698,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 STAMP(4);
             }
             // ==== phase F: chi^2 + decision (tid 0) || next proposal, tile maxima (others) ====
-            // a long tail (the HBM layout: thousands of rays) is summed by the whole
-            // block, exactly in the reference's order (exact_sum.h)
-            double C_big = 0.0;
-            bool big = false;
-            if constexpr (!SMALL) {
-                const int k0 = sh.k0;
-                if (fwd && n - k0 >= kChainExactMin) {
-                    const double C0 = k0 > 0 ? v.prefix[k0 - 1] : 0.0;
-                    big = block_exact_sum<kChainThreads>(v.term + k0, n - k0, C0, v.cprefix + k0, &C_big,
-                                                         *reinterpret_cast<ExactSumLds *>(lds + L.exact));
-                }
-            }
             const long long tF = prof_on ? clock64() : 0;  // diagnostic: per-wave time in F
             double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
             if (wv == 0) {
@@ -721,13 +705,21 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 if (fwd) {
                     // the terms added in k order (MCsub.jl:170-172), bit for bit, by this
                     // wave (exact_sum.h); phase E put the changed rays' new terms in place
-                    // (the old ones wait in cterm).  The last wave may prove meanwhile that
-                    // no remaining sum can be accepted (sh.early_reject): the sum stops.
-                    double C = big ? C_big : (k0 > 0 ? v.prefix[k0 - 1] : 0.0);  // MCsub.jl:169 C = 0
-                    if (!big && k0 < n) {
+                    // (the old ones wait in cterm, their sums in prefix).  Rays in LDS:
+                    // binade-run scans of the tail; rays in HBM (long tails, few changed
+                    // terms): the new sums follow the old ones at a checked constant offset
+                    // between changed rays.  The last wave may prove meanwhile that no
+                    // remaining sum can be accepted (sh.early_reject): the sum stops.
+                    double C = k0 > 0 ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
+                    if (k0 < n) {
                         bool stopped = false;
-                        C = wave_seq_sum(v.term + k0, n - k0, C, v.cprefix + k0, lane, &sh.early_reject, &stopped,
-                                         prof_on ? &sh.prof[65] : nullptr);
+                        long long *rc = prof_on ? &sh.prof[65] : nullptr;
+                        if constexpr (SMALL)
+                            C = wave_seq_sum(v.term + k0, n - k0, C, v.cprefix + k0, lane, &sh.early_reject, &stopped,
+                                             rc);
+                        else
+                            C = wave_delta_sum(v.term + k0, v.prefix + k0, v.rflag + k0, n - k0, C, v.cprefix + k0,
+                                               lane, &sh.early_reject, &stopped, rc);
                         if (prof_on && lane == 0) sh.prof[64] += n - k0;
                     }
                     phi_n = k0 < n ? C : sh.phi;

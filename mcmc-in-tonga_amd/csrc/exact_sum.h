@@ -411,4 +411,96 @@ __device__ __forceinline__ double wave_seq_sum(const double *t, int cnt, double 
     return C;
 }
 
+// ---- one wave: the sequential sum again after a few of its terms changed ----
+// out[k] = C_k, C_k = C_{k-1} + t[k] (C_{-1} = C, the same value before and
+// after the change), given the OLD partial sums old[k] (the same recurrence
+// over the old terms) and chg[k] != 0 where t[k] changed.  Between changed
+// terms the new sum follows the old one at a constant offset D: if old[k-1]
+// and old[k] lie in one binade [2^b, 2^(b+1)), old[k-1] + D and old[k] + D in
+// the same one, and t[k]/u is not a tie (or D/u is even: the same parity), both
+// sums take the same rounded step, so C_k = old[k] + D exactly.  A term where
+// that does not hold, or that changed, is added with an ordinary FP64 add (the
+// reference's operation) and D is re-derived (and checked exact).  Each round
+// checks 64 terms with a few VALU ops and a ballot -- no scan -- so a long tail
+// with few changed terms (the chain after one proposal) costs little more than
+// reading it.  Every lane of the wave calls it with the same arguments; *stop
+// (if given) is polled once per round.
+namespace wdelta {
+__device__ __forceinline__ double shr1_f64(double v, double first) {  // lane l: v of lane l-1; lane 0: first
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v),
+                             f = (unsigned long long)__double_as_longlong(first);
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)f, (int)(unsigned)b, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(f >> 32), (int)(unsigned)(b >> 32), 0x138, 0xf, 0xf,
+                                               false);  // wave_shr:1
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+}  // namespace wdelta
+
+__device__ __forceinline__ double wave_delta_sum(const double *t, const double *old, const int *chg, int cnt,
+                                                 double C, double *out, int lane, const int *stop, bool *stopped,
+                                                 long long *rounds = nullptr) {
+    using namespace wseq;
+    double D = 0.0;                     // new - old at the last settled position (both start at C)
+    double prev_old = C, prev_new = C;  // the old and new sums just before the first unsettled term
+    bool dexact = true;
+    // 64-term windows, the next one in flight
+    auto ld = [&](int p, double &tv, double &ov, int &cv) {
+        const bool in = p + lane < cnt;
+        tv = in ? t[p + lane] : 0.0;
+        ov = in ? old[p + lane] : 0.0;
+        cv = in ? chg[p + lane] : 0;
+    };
+    double tv, ov, tn, on;
+    int cv, cn;
+    ld(0, tv, ov, cv);
+    ld(64, tn, on, cn);
+    for (int base = 0; base < cnt; base += 64) {
+        const int lim = min(64, cnt - base);
+        if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            *stopped = true;
+            return prev_new;
+        }
+        const double op = wdelta::shr1_f64(ov, prev_old);  // old[k - 1] (lane 0: the window's predecessor)
+        const int bo = expo(op), eo = expo(ov);
+        const double inv_u = p2(2098 - min(max(bo, 64), 2000));
+        const double x = tv * inv_u;  // t/u (exact: power-of-two scaling)
+        const bool tie = x - __builtin_floor(x) == 0.5;
+        // what does not depend on the offset (bitwise & |: no branches)
+        const int fixed = (int)(cv == 0) & (int)(bo >= 64) & (int)(bo <= 2000) & (int)(eo == bo) & (int)(tv >= 0.0);
+        int lo = 0;
+        while (true) {  // settle runs at offset D; a failing term is added plainly, D re-derived
+            if (rounds && lane == 0) *rounds += 1;  // diagnostic
+            const double np = op + D, nk = ov + D;  // the new sums at k - 1 and k, if the offset holds
+            const double dq = D * inv_u;            // D/u (exact)
+            const bool dodd = dq - 2.0 * __builtin_floor(dq * 0.5) != 0.0;
+            const bool ok = (fixed & (int)dexact & (int)(expo(np) == bo) & (int)(expo(nk) == bo) &
+                             (int)!(tie && dodd)) != 0;
+            const bool mine = lane >= lo && lane < lim;
+            const unsigned long long bad = __ballot(mine && !ok);
+            const int f = bad ? __builtin_ctzll(bad) : lim;
+            if (out && mine && lane < f) out[base + lane] = nk;
+            if (f == lim) {
+                prev_old = readlane_f64(ov, lim - 1);
+                prev_new = readlane_f64(nk, lim - 1);
+                break;
+            }
+            const double cnm1 = f > lo ? readlane_f64(nk, f - 1) : prev_new;
+            const double cnew = cnm1 + readlane_f64(tv, f);  // the reference's add
+            const double cold = readlane_f64(ov, f);
+            if (out && lane == 0) out[base + f] = cnew;
+            D = cnew - cold;
+            dexact = (cold + D == cnew) && (cnew - D == cold);
+            prev_old = cold;
+            prev_new = cnew;
+            lo = f + 1;
+            if (lo >= lim) break;
+        }
+        tv = tn;
+        ov = on;
+        cv = cn;
+        ld(base + 128, tn, on, cn);
+    }
+    return prev_new;
+}
+
 }  // namespace tdstar

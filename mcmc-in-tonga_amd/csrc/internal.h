@@ -150,6 +150,8 @@ hipError_t launch_nearest_grid(const double *qx, const double *qy, const double 
 
 // Testing: the block-wide exact sequential sum (exact_sum.h) on device buffers.
 hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fallbacks);
+hipError_t test_wave_delta_sum(const double *term, const double *old, const int *chg, int cnt, double C0,
+                               double *prefix, double *C_end);
 hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast);
 
 // ptS[i] = julia_sum_j w[j] * ((0.5*(z0[j]+z0[j+1])) / 1000) per ray (MCsub.jl:147-159).

@@ -268,7 +268,22 @@ __global__ __launch_bounds__(64) void k_test_wave_seq_sum(const double *__restri
     }
 }
 
+__global__ __launch_bounds__(64) void k_test_wave_delta_sum(const double *__restrict__ term,
+                                                            const double *__restrict__ old,
+                                                            const int *__restrict__ chg, int cnt, double C0,
+                                                            double *__restrict__ prefix, double *C_end) {
+    bool stopped = false;
+    const double C = wave_delta_sum(term, old, chg, cnt, C0, prefix, (int)threadIdx.x, nullptr, &stopped);
+    if (threadIdx.x == 0) *C_end = C;
+}
+
 }  // namespace
+
+hipError_t test_wave_delta_sum(const double *term, const double *old, const int *chg, int cnt, double C0,
+                               double *prefix, double *C_end) {
+    hipLaunchKernelGGL(k_test_wave_delta_sum, dim3(1), dim3(64), 0, nullptr, term, old, chg, cnt, C0, prefix, C_end);
+    return hipGetLastError();
+}
 
 hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fallbacks) {
     hipLaunchKernelGGL(k_test_wave_seq_sum, dim3(1), dim3(64), 0, nullptr, term, cnt, C0, prefix, C_end, fallbacks);

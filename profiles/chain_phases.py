@@ -24,12 +24,13 @@ PHASES = ["(loop top)", "B tiles + birth/death query", "C points", "D orphans", 
 def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
+    nrays = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # > 0: synthetic rays (the stress geometry: 10000)
     tt = tonga.load()
-    ds = tt.load_data_Tonga()
+    ds = tt.synthetic_rays(nrays, seed=5) if nrays > 0 else tt.load_data_Tonga()
     ctx = tt.TdContext.from_datastruct(ds)
     prm = tt.define_TDstructrure().replace(max_cells=2 * N)
     ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000, chain=1), tt.random_model(N, 3))
-    ch.run(2000)
+    ch.run(2000 if nrays == 0 else 200)
     L = tt.lib()
     out0 = (ctypes.c_int64 * 72)()
     L.tdt_chain_profile(ch.h, 1, out0)

@@ -115,3 +115,74 @@ def test_wave_sum_binade_walk(tt):
     check(tt, np.concatenate([base[:70], [np.nan], base[70:90]]), 3.0)
     check(tt, np.full(130, 2.0 ** 60), 2.0 ** 62)            # huge, exact ties
     check(tt, rng.exponential(1e-300, 200), 1e-310)            # subnormal start
+
+
+def delta_run(tt, terms, old_prefix, changed, c0):
+    terms = np.ascontiguousarray(terms, dtype=np.float64)
+    old_prefix = np.ascontiguousarray(old_prefix, dtype=np.float64)
+    changed = np.ascontiguousarray(changed, dtype=np.int32)
+    pre = np.zeros(len(terms))
+    ce = ctypes.c_double()
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    assert tt.lib().tdt_wave_delta_sum(0, P(terms), P(old_prefix), changed.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                       len(terms), float(c0), P(pre), ctypes.byref(ce)) == 0
+    return pre, ce.value
+
+
+def delta_check(tt, old_terms, new_terms, c0):
+    changed = (old_terms != new_terms).astype(np.int32)
+    old_prefix = seq(old_terms, c0)
+    want = seq(new_terms, c0)
+    pre, ce = delta_run(tt, new_terms, old_prefix, changed, c0)
+    same = (pre == want) | (np.isnan(pre) & np.isnan(want))
+    bad = np.nonzero(~same)[0]
+    assert len(bad) == 0, (bad[:5], pre[bad[:5]], want[bad[:5]])
+    assert ce == want[-1] or (np.isnan(ce) and np.isnan(want[-1]))
+
+
+def test_delta_sum_chain_like(tt):
+    """The chain's case: a tail of chi^2 terms of which a few changed."""
+    rng = np.random.default_rng(21)
+    for trial in range(40):
+        n = int(rng.choice([1, 5, 63, 64, 65, 381, 1000, 5000]))
+        old = rng.exponential(36.0, n)
+        new = old.copy()
+        idx = rng.choice(n, size=min(n, int(rng.integers(1, 30))), replace=False)
+        new[idx] = old[idx] * rng.uniform(0.2, 3.0, len(idx))
+        c0 = float(rng.choice([0.0, 1.0, 3000.0, 8191.9, 8192.0, 1e5]))
+        delta_check(tt, old, new, c0)
+
+
+def test_delta_sum_adversarial(tt):
+    rng = np.random.default_rng(22)
+    base = rng.exponential(36.0, 600)
+    # ties everywhere (terms with a set bit just below the unit), offsets odd and even
+    ties = (rng.integers(1, 9, 600) * 2 + 1) * 2.0 ** -34
+    for d in (2.0 ** -38, 3 * 2.0 ** -38, 1.0, -0.5, 1e-3):
+        new = ties.copy()
+        new[0] += d
+        delta_check(tt, ties, new, 5000.0)
+    # the new sum crosses binades the old one does not (and back)
+    new = base.copy()
+    new[3] += 9000.0
+    delta_check(tt, base, new, 100.0)
+    new = base.copy()
+    new[3] = 0.0
+    delta_check(tt, base, new, 8100.0)
+    # huge relative changes (inexact offsets), zeros, NaN / inf terms
+    new = base.copy()
+    new[5] = 1e12
+    delta_check(tt, base, new, 0.0)
+    new = base.copy()
+    new[[7, 300]] = [np.inf, 1.0]
+    delta_check(tt, base, new, 10.0)
+    new = base.copy()
+    new[9] = np.nan
+    delta_check(tt, base, new, 10.0)
+    z = np.zeros(300)
+    new = z.copy()
+    new[100] = 5.0
+    delta_check(tt, z, new, 0.0)
+    # every term changed / none changed
+    delta_check(tt, base, base * 1.0000001, 50.0)
+    delta_check(tt, base, base.copy(), 50.0)
