@@ -39,7 +39,8 @@ struct ChainScalars {
     int64_t bytes;         // algorithmic global-memory bytes the proposals needed (roofline)
     int64_t prof[kProfSlots];  // diagnostic (DevChain::profile): cycles per phase [0..13], [14] proven
                                // rejections, [15] grid fallbacks, [16 + 10 (action-1) + j] per-action phases,
-                               // [56 + wave] phase F per wave, [64] chi^2 tail terms, [65] chi^2 scan rounds
+                               // [56 + wave] phase F per wave, [64] chi^2 tail terms, [65] chi^2 scan rounds,
+                               // [66..67] wave-0 F timeline, [68..71] tiles hit, points seen/changed, rays changed
     int ncells;            // cells in the model
     int nslots;            // slot high-water mark
     int nfree;             // free-slot stack depth

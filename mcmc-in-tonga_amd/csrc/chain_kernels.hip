@@ -761,6 +761,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     grid_prefetch(d, sh, lane, action, action == tdchain::kBirth ? new_slot : slot_k, kx, ky,
                                   kz, pp.x, pp.y, pp.z);
             } else if (wv == kWaves - 2) {
+                if (prof_on && lane == 0) {  // diagnostic: work sizes
+                    sh.prof[68] += sh.n_tiles;
+                    sh.prof[69] += sh.pts_seen;
+                    sh.prof[70] += sh.n_changed;
+                    sh.prof[71] += sh.n_rays;
+                }
                 if (lane == 0 && fwd) {  // accounting, off wave 0's path
                     atomicAdd((unsigned long long *)&sh.evaluations, 1ull);
                     // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),

@@ -69,6 +69,8 @@ def main():
     ev = max(sum(prop), 1)
     res["chi2 tail terms per proposal"] = round((out[64] - out0[64]) / ev, 1)
     res["chi2 scan rounds per proposal"] = round((out[65] - out0[65]) / ev, 2)
+    res["per evaluated proposal: tiles hit, points seen, points changed, rays changed"] = [
+        round((out[k] - out0[k]) / ev, 1) for k in (68, 69, 70, 71)]
     res["F wave 0: cycles to scan end / to decision (per iter)"] = [round((out[k] - out0[k]) / iters, 1)
                                                                      for k in (66, 67)]
     print(json.dumps(res, indent=1))
