@@ -37,7 +37,7 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
  * phases split by action (j: A..F, commit, next proposal, final barrier),
  * [56 + w] phase F of wave w, [64] chi^2 tail terms, [65] chi^2 scan rounds.
  * Never enabled in measured runs. */
-int tdt_chain_profile(td_chain *ch, int enable, int64_t out[72]);
+int tdt_chain_profile(td_chain *ch, int enable, int64_t out[80]);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);
@@ -61,6 +61,16 @@ int tdt_exact_sum(int device, const double *term, int64_t cnt, double C0, double
  * where term[k] differs from the old term.  Needs a GPU. */
 int tdt_wave_delta_sum(int device, const double *term, const double *old_prefix, const int *changed, int64_t cnt,
                        double C0, double *prefix, double *C_end);
+/* The chain's chi^2 walk (exact_sum.h delta_marks / delta_walk / delta_remark /
+ * delta_commit, one 512-thread workgroup): old_prefix[0..n) are the partial
+ * sums of term_old (C_{-1} = 0), term[k0..n) the new terms, changed[k] != 0
+ * where they differ; prefix = the new partial sums (old ones before k0), C_end
+ * = prefix[n-1], events = the terms the walk added one by one, mask_ok = the
+ * event words kept across the proposal equal those of the new state.
+ * n <= 65536. */
+int tdt_block_delta_sum(int device, const double *term, const double *term_old, const double *old_prefix,
+                        const int *changed, int64_t k0, int64_t n, double *prefix, double *C_end, int64_t *events,
+                        int *mask_ok);
 int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, double *prefix, double *C_end,
                      int *fallbacks);
 

@@ -82,6 +82,8 @@ SIGNATURES = {
     "tdt_chain_set_lds_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_exact_sum": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _d, _pd, _pd, _pi32]),
     "tdt_wave_delta_sum": (ctypes.c_int, [ctypes.c_int, _pd, _pd, _pi32, _i64, _d, _pd, _pd]),
+    "tdt_block_delta_sum": (ctypes.c_int, [ctypes.c_int, _pd, _pd, _pd, _pi32, _i64, _i64, _pd, _pd,
+                                            ctypes.POINTER(ctypes.c_int64), _pi32]),
     "tdt_wave_seq_sum": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _d, _pd, _pd, _pi32]),
     "tdt_accept": (ctypes.c_int, [ctypes.POINTER(TdChainParams), ctypes.c_int, _d, _d, _i64, _d, _d, _d, _d, _d]),
 }

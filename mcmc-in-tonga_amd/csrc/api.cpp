@@ -533,6 +533,37 @@ int tdt_wave_delta_sum(int device, const double *term, const double *old_prefix,
     return e == hipSuccess ? TD_OK : TD_ERR_HIP;
 }
 
+int tdt_block_delta_sum(int device, const double *term, const double *term_old, const double *old_prefix,
+                        const int *changed, int64_t k0, int64_t n, double *prefix, double *C_end, int64_t *events,
+                        int *mask_ok) {
+    if (!term || !term_old || !old_prefix || !changed || !prefix || !C_end || !events || !mask_ok || n < 1 ||
+        n > 64 * 1024 || k0 < 0 || k0 > n)
+        return TD_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return TD_ERR_HIP;
+    const size_t nb = sizeof(double) * (size_t)n;
+    void *buf = nullptr;
+    if (hipMalloc(&buf, 4 * nb + 3 * sizeof(double) + sizeof(int) * (size_t)n) != hipSuccess) return TD_ERR_NOMEM;
+    double *dt = static_cast<double *>(buf), *dto = dt + n, *dold = dto + n, *dcp = dold + n, *de = dcp + n;
+    long long *dev = reinterpret_cast<long long *>(de + 1);
+    int *dok = reinterpret_cast<int *>(de + 2);
+    int *dc = reinterpret_cast<int *>(de + 3);
+    hipError_t e = hipMemcpy(dt, term, nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dto, term_old, nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dold, old_prefix, nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dc, changed, sizeof(int) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(dcp, 0xff, nb);  // NaN: a COPY segment that was not written shows
+    if (e == hipSuccess) e = test_block_delta(dt, dto, dold, dc, (int)k0, (int)n, dcp, de, dev, dok);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(prefix, dold, nb, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(C_end, de, sizeof(double), hipMemcpyDeviceToHost);
+    long long ev = 0;
+    if (e == hipSuccess) e = hipMemcpy(&ev, dev, sizeof(long long), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(mask_ok, dok, sizeof(int), hipMemcpyDeviceToHost);
+    *events = ev;
+    (void)hipFree(buf);
+    return e == hipSuccess ? TD_OK : TD_ERR_HIP;
+}
+
 int tdt_set_nn_method(td_ctx *ctx, int method) {
     if (!ctx || method < 0 || method > 2) return TD_ERR_ARG;
     ctx->nn_method = method;

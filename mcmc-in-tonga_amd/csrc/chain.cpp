@@ -584,7 +584,7 @@ int tdt_chain_set_lds_mode(td_chain *ch, int mode) {
     return TD_OK;
 }
 
-int tdt_chain_profile(td_chain *ch, int enable, int64_t out[72]) {
+int tdt_chain_profile(td_chain *ch, int enable, int64_t out[80]) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE) return TD_ERR_ARG;
     ch->dev.profile = enable;
     if (out) {

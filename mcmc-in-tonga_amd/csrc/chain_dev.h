@@ -26,7 +26,7 @@
 namespace tdstar {
 
 constexpr int kTilePts = 16;
-constexpr int kProfSlots = 72;
+constexpr int kProfSlots = 80;
 constexpr int kChainThreads = 512;  // 8 waves: 256 VGPRs per lane, no spills
 constexpr int kBucketCap = 32;
 
@@ -40,7 +40,9 @@ struct ChainScalars {
     int64_t prof[kProfSlots];  // diagnostic (DevChain::profile): cycles per phase [0..13], [14] proven
                                // rejections, [15] grid fallbacks, [16 + 10 (action-1) + j] per-action phases,
                                // [56 + wave] phase F per wave, [64] chi^2 tail terms, [65] chi^2 scan rounds,
-                               // [66..67] wave-0 F timeline, [68..71] tiles hit, points seen/changed, rays changed
+                               // [66..67] wave-0 F timeline, [68..71] tiles hit, points seen/changed, rays changed,
+                               // [72..75] chi^2 walk (rays in HBM): events, batch-load cycles, event-walk
+                               // cycles, terms added one by one
     int ncells;            // cells in the model
     int nslots;            // slot high-water mark
     int nfree;             // free-slot stack depth

@@ -136,6 +136,7 @@ struct Shared {
     int grid_fallbacks32;  // grid searches that needed the full scan
     int grid_ovf;          // LDS copy of *d.grid_overflow
     OrphanRec orph[kOrphanLds];
+    DeltaSegs dseg;  // rays in HBM: phase F's new chi^2 partial sums as segments over the old ones
     long long prof[kProfSlots], t_last, t_iter;  // diagnostic phase stamps
 };
 
@@ -154,7 +155,7 @@ struct Shared {
 
 // LDS carve-up (host and device agree on it through this function).
 struct LdsPlan {
-    size_t scratch, draws, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
+    size_t scratch, draws, smask, cmask, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
         tS, sig, rflag, rhit, ord, total;
 };
 
@@ -185,6 +186,9 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
         L.rflag = o; o += align16(sizeof(int) * n);
         L.rhit = o; o += align16(sizeof(int) * n);
         L.ord = o; o += align16(sizeof(int) * cap);
+    } else {  // the chi^2 walk's event words (exact_sum.h): static ones, kept; changed rays
+        L.smask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
+        L.cmask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
     }
     L.total = o;
     return L;
@@ -532,8 +536,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.grid_ovf = *d.grid_overflow;
         for (int k = 0; k < kProfSlots; ++k) sh.prof[k] = 0;
         sh.t_last = clock64();
+        sh.dseg.nseg = 0;
     }
     __syncthreads();
+    unsigned long long *smask = reinterpret_cast<unsigned long long *>(lds + L.smask);
+    unsigned long long *cmask = reinterpret_cast<unsigned long long *>(lds + L.cmask);
+    if constexpr (!SMALL) {  // rays in HBM: the chi^2 walk's static event words of the current state
+        delta_marks(v.term, v.prefix, nullptr, n, smask, wv, delta_words(n), kWaves, lane);
+        for (int w = tid; w < delta_words(n); w += kChainThreads) cmask[w] = 0ull;
+        __syncthreads();
+    }
 
     // the draws (and their normal quantiles) of 64 iterations, one lane each:
     // a function of (seed, chain, iteration) only; and the first proposal
@@ -558,8 +570,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const long long iter0 = sh.iter;
     double phi_r = sh.phi;
     int cur_r = 0;
+    bool pend_r = false;  // rays in HBM: an accepted proposal's chi^2 partial sums not yet written
     for (long long it = 0; it < iters; ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
+        if constexpr (!SMALL) {
+            // the previous accepted proposal's partial sums (read again only in phase F,
+            // after at least one barrier): off its critical path, before this one's tiles
+            if (pend_r) delta_commit<16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
+            pend_r = false;
+        }
         bool acc_r = false;
         const PState &cur = sh.ps[sh.cur];
         const Proposal p = cur.p;
@@ -582,11 +601,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 const bool q1 = action == tdchain::kBirth || action == tdchain::kMove;  // new site
                 const TileQuery tq0 = tile_query(kx, ky, kz), tq1 = tile_query(p.x, p.y, p.z);
                 const int nthr = query ? kChainThreads - 64 : kChainThreads;
+                // tiles in flight per thread: LDS latency is short; HBM needs more
+                constexpr int TU = SMALL ? 3 : 8;
                 if (tid < nthr)
-                    for (int t0 = tid; t0 < NT; t0 += 3 * nthr) {  // three tiles in flight per thread
-                        bool hit[3];
+                    for (int t0 = tid; t0 < NT; t0 += TU * nthr) {
+                        bool hit[TU];
 #pragma unroll
-                        for (int u = 0; u < 3; ++u) {
+                        for (int u = 0; u < TU; ++u) {
                             const int t = min(t0 + u * nthr, NT - 1);  // clamped: loads stay unconditional
                             const float thr = tile_thr(v.tmaxd[t]);
                             const bool h0 = tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr);
@@ -594,7 +615,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                             hit[u] = t0 + u * nthr < NT && ((q0 && h0) || (q1 && h1));
                         }
 #pragma unroll
-                        for (int u = 0; u < 3; ++u)
+                        for (int u = 0; u < TU; ++u)
                             if (hit[u]) v.thit[atomicAdd(&sh.n_tiles, 1)] = t0 + u * nthr;
                     }
             }
@@ -692,6 +713,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         v.cterm[r] = v.term[r];                      // kept to undo a rejection
                         v.term[r] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                         atomicAdd(&sh.ray_pts, npr);
+                        if constexpr (!SMALL) atomicOr(&cmask[r >> 6], 1ull << (r & 63));  // an event of the walk
                     }
                 }
                 __syncthreads();
@@ -706,20 +728,20 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     // the terms added in k order (MCsub.jl:170-172), bit for bit, by this
                     // wave (exact_sum.h); phase E put the changed rays' new terms in place
                     // (the old ones wait in cterm, their sums in prefix).  Rays in LDS:
-                    // binade-run scans of the tail; rays in HBM (long tails, few changed
-                    // terms): the new sums follow the old ones at a checked constant offset
-                    // between changed rays.  The last wave may prove meanwhile that no
-                    // remaining sum can be accepted (sh.early_reject): the sum stops.
+                    // binade-run scans of the tail, and the last wave may prove meanwhile
+                    // that no remaining sum can be accepted (sh.early_reject): the sum
+                    // stops.  Rays in HBM (long tails, few changed terms): the new sums
+                    // follow the old ones at a checked constant offset between events.
                     double C = k0 > 0 ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
                     if (k0 < n) {
                         bool stopped = false;
-                        long long *rc = prof_on ? &sh.prof[65] : nullptr;
+                        long long *rc = prof_on && SMALL ? &sh.prof[65] : nullptr;
                         if constexpr (SMALL)
                             C = wave_seq_sum(v.term + k0, n - k0, C, v.cprefix + k0, lane, &sh.early_reject, &stopped,
                                              rc);
-                        else
-                            C = wave_delta_sum(v.term + k0, v.prefix + k0, v.rflag + k0, n - k0, C, v.cprefix + k0,
-                                               lane, &sh.early_reject, &stopped, rc);
+                        else  // O(events), not O(tail): exact_sum.h delta_walk
+                            C = delta_walk(v.term, v.prefix, v.rflag, k0, n, C, smask, cmask, v.cprefix, sh.dseg, lane,
+                                           prof_on ? &sh.prof[72] : nullptr);
                         if (prof_on && lane == 0) sh.prof[64] += n - k0;
                     }
                     phi_n = k0 < n ? C : sh.phi;
@@ -786,7 +808,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // non-negative terms is within n ulps of any other association; above
                 // the rejection bound by a wide margin, the proposal is rejected
                 const int k0 = sh.k0;
-                if (fwd && k0 < n) {
+                if (SMALL && fwd && k0 < n) {
                     double part = 0.0;
                     for (int k = k0 + lane; k < n; k += 64) part = part + v.term[k];
                     const double S = wave_sum_f64(part);
@@ -836,7 +858,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     v.ptS[r] = v.cptS[r];
                     v.rflag[r] = 0;
                 }
-                for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
+                if constexpr (SMALL) {
+                    for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
+                } else if (fwd && k0 < n) {
+                    pend_r = true;  // written at the top of the next iteration
+                    if (wv == 1) delta_remark(v.term, v.prefix, v.cprefix, n, sh.dseg, smask, lane);
+                }
                 if (action == tdchain::kDeath)  // deleteat!: positions after the killed one shift down
                     for (int j = (int)pp.index + 1 + tid; j < ncells; j += kChainThreads) {
                         const int s = d.order_tmp[j];
@@ -935,6 +962,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         STAMP(6);
     }
 
+    if constexpr (!SMALL)
+        if (pend_r) delta_commit<16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
     // ---- leave the LDS copies behind (flags and grid are already clean) ----
     if constexpr (SMALL) {
         for (int i = tid; i < NT; i += kChainThreads) d.tile_maxd[i] = v.tmaxd[i];

@@ -436,13 +436,15 @@ __device__ __forceinline__ double shr1_f64(double v, double first) {  // lane l:
 }
 }  // namespace wdelta
 
-__device__ __forceinline__ double wave_delta_sum(const double *t, const double *old, const int *chg, int cnt,
-                                                 double C, double *out, int lane, const int *stop, bool *stopped,
-                                                 long long *rounds = nullptr) {
+// wave_delta_run: the same from different sums before the first term
+// (prev_old = old[-1], prev_new = the new sum there); wave_delta_sum starts
+// both at C.
+__device__ __forceinline__ double wave_delta_run(const double *t, const double *old, const int *chg, int cnt,
+                                                 double prev_old, double prev_new, double *out, int lane,
+                                                 const int *stop, bool *stopped, long long *rounds = nullptr) {
     using namespace wseq;
-    double D = 0.0;                     // new - old at the last settled position (both start at C)
-    double prev_old = C, prev_new = C;  // the old and new sums just before the first unsettled term
-    bool dexact = true;
+    double D = prev_new - prev_old;  // new - old at the last settled position
+    bool dexact = (prev_old + D == prev_new) && (prev_new - D == prev_old);
     // 64-term windows, the next one in flight
     auto ld = [&](int p, double &tv, double &ov, int &cv) {
         const bool in = p + lane < cnt;
@@ -501,6 +503,392 @@ __device__ __forceinline__ double wave_delta_sum(const double *t, const double *
         ld(base + 128, tn, on, cn);
     }
     return prev_new;
+}
+
+__device__ __forceinline__ double wave_delta_sum(const double *t, const double *old, const int *chg, int cnt,
+                                                 double C, double *out, int lane, const int *stop, bool *stopped,
+                                                 long long *rounds = nullptr) {
+    return wave_delta_run(t, old, chg, cnt, C, C, out, lane, stop, stopped, rounds);
+}
+
+// ---- the whole block: the sequential sum again, walking only its events ----
+// The same problem as wave_delta_sum (new terms t, OLD partial sums old),
+// split so its cost follows the number of changed terms rather than the length
+// of the tail.  A term k is an EVENT when its step cannot be inferred from the
+// old sums whatever the offset: it changed, it is not >= 0, old[k-1] and
+// old[k] lie in different binades (or outside [2^-959, 2^977]), or t/u is a
+// tie.  Between two events every old partial sum lies in ONE binade b, so a
+// constant offset D = new - old (a multiple of u = 2^(b-52), checked exact)
+// carries over the whole run exactly when the run's first and last shifted
+// sums stay in binade b (the shifted sums are monotone): two checks per run
+// instead of one per term.  An event is added with an ordinary FP64 add (the
+// reference's operation, MCsub.jl:172) and re-derives D.  A run that fails its
+// checks (rare: the new sum crosses a binade the old one does not) is handed
+// to wave_delta_run, term by term.
+//   delta_marks : the STATIC event bits (everything but "changed") of 64-term
+//                 words; the chain keeps them across proposals (delta_remark);
+//   delta_walk  : one wave walks the events in order (64 at a time: their
+//                 positions from the words OR the changed-term words, their
+//                 old sums and terms in one round of loads) and records the
+//                 new sums as segments: OFFSET (old + D), VALUE (one event's
+//                 sum) or COPY (written to out by wave_delta_run);
+//   delta_remark: after an accepted proposal, the static bits that can change:
+//                 around VALUE events and inside COPY segments (an OFFSET run
+//                 stays in its binade, so its bits stand);
+//   delta_commit: the block applies the segments to old in place.
+constexpr int kDeltaSegCap = 128;
+constexpr int kSegOffset = 0, kSegValue = 1, kSegCopy = 2;
+constexpr int kSegPosMask = (1 << 29) - 1;
+
+struct DeltaSegs {
+    int sm[kDeltaSegCap];  // start | mode << 29
+    double v[kDeltaSegCap];  // OFFSET: D, VALUE: the sum
+    int evbuf[64];           // event positions of the batch being walked
+    int nseg, k0;
+};
+
+__host__ __device__ __forceinline__ int delta_words(int n) { return (n + 63) >> 6; }
+
+// the static event bit of term k: t = t[k], pm = old[k-1] (0 for k = 0), pk = old[k]
+__device__ __forceinline__ bool delta_static_event(double t, double pm, double pk) {
+    using namespace wseq;
+    const int bo = expo(pm), eo = expo(pk);
+    const double x = t * p2(2098 - min(max(bo, 64), 2000));  // t/u (exact)
+    const bool tie = x - __builtin_floor(x) == 0.5;
+    return !((t >= 0.0) & (bo == eo) & (bo >= 64) & (bo <= 2000) & !tie);
+}
+
+// Event words w_first, w_first + w_step, ... below w_end (one wave per call);
+// chg (nullable) adds the changed terms.
+__device__ __forceinline__ void delta_marks(const double *t, const double *old, const int *chg, int n,
+                                            unsigned long long *mask, int w_first, int w_end, int w_step, int lane) {
+    constexpr int U = 4;  // words in flight
+    for (int w0 = w_first; w0 < w_end; w0 += U * w_step) {
+        double tv[U], ov[U], pv[U];
+        int cv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = min(64 * (w0 + u * w_step) + lane, n - 1);  // clamped: loads stay unconditional
+            tv[u] = t[k];
+            ov[u] = old[k];
+            pv[u] = old[max(k - 1, 0)];
+            cv[u] = chg ? chg[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int w = w0 + u * w_step;
+            const int k = 64 * w + lane;
+            const bool ev = delta_static_event(tv[u], k > 0 ? pv[u] : 0.0, ov[u]) | (cv[u] != 0);
+            const unsigned long long m = __ballot(k < n && ev);
+            if (w < w_end && lane == 0) mask[w] = m;
+        }
+    }
+}
+
+// One wave, every lane with the same arguments; C0 = the sum before k0 (old
+// and new alike); the events are the bits of smask | cmask from k0 on (cmask
+// nullable; its words are cleared as they are read).  Returns the new sum
+// through n-1; sg holds the segments.
+__device__ double delta_walk(const double *t, const double *old, const int *chg, int k0, int n, double C0,
+                             const unsigned long long *smask, unsigned long long *cmask, double *out, DeltaSegs &sg,
+                             int lane, long long *diag = nullptr) {
+    // diag (diagnostic, nullable): [0] events, [1] cycles in batch loads, [2] cycles walking
+    // events, [3] terms added by wave_delta_run
+    using namespace wseq;
+    const int w0 = k0 >> 6, W = delta_words(n);
+    double prev_old = C0, prev_new = C0;  // the sums just before p
+    int p = k0, nseg = 0;
+    bool mat = false;  // the segment table is full: the rest goes to out
+    auto seg = [&](int start, int mode, double v) -> bool {  // false: write out[] instead
+        if (mat) return false;
+        if (nseg == kDeltaSegCap - 1) {
+            mat = true;
+            mode = kSegCopy;
+        }
+        if (lane == 0) {
+            sg.sm[nseg] = start | (mode << 29);
+            sg.v[nseg] = v;
+        }
+        ++nseg;
+        return !mat;
+    };
+    auto offset_run = [&](int e, double D) {  // [p, e) at offset D
+        if (!seg(p, kSegOffset, D))
+            for (int k = p + lane; k < e; k += 64) out[k] = old[k] + D;
+    };
+    auto run = [&](int s, double cend) {  // the run [p, s), old[s-1] = cend
+        const int b = expo(cend);         // every old sum of the run lies in binade b
+        while (p < s) {
+            const double D = prev_new - prev_old;
+            const bool dex = (prev_old + D == prev_new) && (prev_new - D == prev_old);
+            const int bn = expo(prev_new);
+            if (dex && bn == b && expo(cend + D) == b) {  // the whole rest at offset D
+                offset_run(s, D);
+                prev_new = cend + D;
+                prev_old = cend;
+                p = s;
+                return;
+            }
+            if (dex && bn == b) {
+                // the new sums leave binade b before the old ones (D > 0): the offset
+                // holds up to the first k with old[k] + D outside b, the rest of the
+                // run is added term by term (one window of loads)
+                const int k = s - 64 + lane;
+                const double ow = old[max(k, 0)], tw = t[max(k, 0)];
+                const unsigned long long bad = __ballot(k >= p && expo(ow + D) != b);
+                const int fl = __builtin_ctzll(bad);  // lane 63 (k = s - 1) fails
+                const int f = s - 64 + fl;
+                if (fl > 0 || f == p) {
+                    double C = prev_new;
+                    if (f > p) {
+                        offset_run(f, D);
+                        C = readlane_f64(ow, fl - 1) + D;
+                    }
+                    seg(f, kSegCopy, 0.0);
+                    if (diag && lane == 0) diag[3] += s - f;
+                    for (int i = fl; i < 64; ++i) {
+                        C = C + readlane_f64(tw, i);  // the reference's add
+                        if (lane == 0) out[s - 64 + i] = C;
+                    }
+                    prev_new = C;
+                    prev_old = cend;
+                    p = s;
+                    return;
+                }
+            } else if (dex && bn < b && prev_new >= 0.0) {
+                // the new sum has not reached binade b yet (D < 0): term by term until it
+                // does (one window of loads per 64 terms), then the offset again
+                const int cnt = min(64, s - p);
+                const int k = min(p + lane, s - 1);
+                const double ow = old[k], tw = t[k];
+                seg(p, kSegCopy, 0.0);
+                double C = prev_new, O = prev_old;
+                int i = 0;
+                for (; i < cnt; ++i) {
+                    C = C + readlane_f64(tw, i);  // the reference's add
+                    O = readlane_f64(ow, i);
+                    if (lane == 0) out[p + i] = C;
+                    if (expo(C) >= b) break;
+                }
+                const int used = i < cnt ? i + 1 : cnt;
+                if (diag && lane == 0) diag[3] += used;
+                prev_new = C;
+                prev_old = O;
+                p += used;
+                continue;
+            }
+            // anything else (rare): term by term to the end of the run
+            seg(p, kSegCopy, 0.0);
+            if (diag && lane == 0) diag[3] += s - p;
+            prev_new = wave_delta_run(t + p, old + p, chg + p, s - p, prev_old, prev_new, out + p, lane, nullptr,
+                                      nullptr);
+            prev_old = cend;
+            p = s;
+        }
+    };
+    auto event = [&](int s, double os, double ts) {
+        const double cnew = prev_new + ts;  // the reference's add
+        if (!seg(s, kSegValue, cnew) && lane == 0) out[s] = cnew;
+        prev_old = os;
+        prev_new = cnew;
+        p = s + 1;
+    };
+    for (int wb = w0; wb < W; wb += 64) {  // 64 words = 4096 terms at a time
+        const int wi = wb + lane;
+        unsigned long long m = 0ull;
+        if (wi < W) {
+            m = smask[wi];
+            if (cmask) {
+                m |= cmask[wi];
+                cmask[wi] = 0ull;
+            }
+            if (wi == w0) m &= ~0ull << (k0 & 63);
+        }
+        const int pc = __popcll(m);
+        const int incl = (int)wave_scan_f64((double)pc);
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        if (tot == 0) continue;
+        if (tot <= 64) {
+            int e = incl - pc;
+            for (unsigned long long mm = m; mm; mm &= mm - 1) sg.evbuf[e++] = 64 * wi + __builtin_ctzll(mm);
+            wave_sync_lds();
+            const long long c0 = diag ? clock64() : 0;
+            const int sl = lane < tot ? sg.evbuf[lane] : k0;
+            const double os = old[sl], om = old[max(sl - 1, 0)], ts = t[sl];  // one round of loads
+            wave_sync_lds();  // evbuf read before the next batch rewrites it
+            long long c1 = 0;
+            if (diag) {
+                const double probe = os + om + ts;  // wait for the loads
+                c1 = clock64();
+                if (lane == 0) {
+                    diag[0] += tot;
+                    diag[1] += c1 - c0 + (probe == 1.2345e300 ? 1 : 0);
+                }
+            }
+            // Speculative pass: every run at its offset (3 dependent adds per event),
+            // lane j keeping what event j saw; then all runs checked at once; the
+            // events before the first failed check stand, the rest go the slow way.
+            double pnv = 0.0, pov = 0.0, cv = 0.0;
+            int hasv = 0;
+            {
+                double pn = prev_new, po = prev_old;
+                int pp = p;
+                for (int j = 0; j < tot; ++j) {
+                    const int sj = __builtin_amdgcn_readlane(sl, j);
+                    const double omj = readlane_f64(om, j), tsj = readlane_f64(ts, j), osj = readlane_f64(os, j);
+                    const bool has = sj > pp;
+                    const double pr = has ? omj + (pn - po) : pn;  // new sum at s - 1
+                    const double c = pr + tsj;                     // the reference's add
+                    if (lane == j) {
+                        pnv = pn;
+                        pov = po;
+                        cv = c;
+                        hasv = has;
+                    }
+                    po = osj;
+                    pn = c;
+                    pp = sj + 1;
+                }
+            }
+            const double Dv = pnv - pov;
+            const int bj = expo(om);
+            const bool okj = !hasv || ((pov + Dv == pnv) && (pnv - Dv == pov) && expo(pnv) == bj &&
+                                       expo(om + Dv) == bj);
+            const unsigned long long badm = __ballot(lane < tot && !okj);
+            const int f = badm ? __builtin_ctzll(badm) : tot;
+            // segments of the confirmed events: [run at its offset,] the event's sum
+            const int cnt_j = lane < f ? hasv + 1 : 0;
+            const int seg_incl = (int)wave_scan_f64((double)cnt_j);
+            const int nnew = __builtin_amdgcn_readlane(seg_incl, 63);
+            int j0 = 0;
+            if (f > 0 && !mat && nseg + nnew < kDeltaSegCap - 1) {
+                const int prev_s = __shfl_up(sl, 1);
+                const int start = lane == 0 ? p : prev_s + 1;
+                int o = nseg + seg_incl - cnt_j;
+                if (lane < f) {
+                    if (hasv) {
+                        sg.sm[o] = start | (kSegOffset << 29);
+                        sg.v[o] = Dv;
+                        ++o;
+                    }
+                    sg.sm[o] = sl | (kSegValue << 29);
+                    sg.v[o] = cv;
+                }
+                nseg += nnew;
+                prev_new = readlane_f64(cv, f - 1);
+                prev_old = readlane_f64(os, f - 1);
+                p = __builtin_amdgcn_readlane(sl, f - 1) + 1;
+                j0 = f;
+            }
+            for (int j = j0; j < tot; ++j) {
+                const int s = __builtin_amdgcn_readlane(sl, j);
+                run(s, readlane_f64(om, j));
+                event(s, readlane_f64(os, j), readlane_f64(ts, j));
+            }
+            if (diag && lane == 0) diag[2] += clock64() - c1;
+        } else {  // dense events (tiny sums, or every term changed): term by term
+            const int e = min(n, 64 * (wb + 64));
+            if (diag && lane == 0) diag[3] += e - p;
+            seg(p, kSegCopy, 0.0);
+            prev_new = wave_delta_run(t + p, old + p, chg + p, e - p, prev_old, prev_new, out + p, lane, nullptr,
+                                      nullptr);
+            prev_old = old[e - 1];
+            p = e;
+        }
+    }
+    if (p < n) run(n, old[n - 1]);
+    if (lane == 0) {
+        sg.nseg = nseg;
+        sg.k0 = k0;
+    }
+    return prev_new;
+}
+
+// The new partial sum at k (k0 - 1 <= k < n) from the segments: k lies in
+// segment i (i = -1: before the tail, unchanged).
+__device__ __forceinline__ double delta_new_at(const double *old, const double *out, const DeltaSegs &sg, int i,
+                                               int k) {
+    if (k < 0) return 0.0;
+    if (i < 0) return old[k];
+    const int mode = sg.sm[i] >> 29;
+    return mode == kSegOffset ? old[k] + sg.v[i] : mode == kSegValue ? sg.v[i] : out[k];
+}
+
+// After an accepted proposal (before delta_commit): the static event bits of
+// the new state (t = the new terms) where they can differ from the old ones.
+// One wave.
+__device__ void delta_remark(const double *t, const double *old, const double *out, int n, const DeltaSegs &sg,
+                             unsigned long long *smask, int lane) {
+    const int nseg = sg.nseg;
+    auto set_bit = [&](int k, bool ev) {
+        const unsigned long long b = 1ull << (k & 63);
+        if (ev) atomicOr(&smask[k >> 6], b);
+        else atomicAnd(&smask[k >> 6], ~b);
+    };
+    // VALUE events, one per lane: the bits at s and s + 1
+    for (int i0 = 0; i0 < nseg; i0 += 64) {
+        const int i = i0 + lane;
+        const int sm = i < nseg ? sg.sm[i] : 0;
+        if (i < nseg && (sm >> 29) == kSegValue) {
+            const int s = sm & kSegPosMask;
+            const double pm = delta_new_at(old, out, sg, i - 1, s - 1);
+            const double ps = sg.v[i];
+            set_bit(s, delta_static_event(t[s], pm, ps));
+            if (s + 1 < n) set_bit(s + 1, delta_static_event(t[s + 1], ps, delta_new_at(old, out, sg, i + 1, s + 1)));
+        }
+    }
+    // COPY segments (rare): every bit of [a, b], b the next segment's start
+    for (int i = 0; i < nseg; ++i) {
+        const int sm = sg.sm[i];
+        if ((sm >> 29) != kSegCopy) continue;
+        const int a = sm & kSegPosMask, b = i + 1 < nseg ? (sg.sm[i + 1] & kSegPosMask) : n;
+        for (int k = a + lane; k <= min(b, n - 1); k += 64) {
+            const double pm = k == a ? delta_new_at(old, out, sg, i - 1, k - 1) : out[k - 1];
+            const double pk = k == b ? delta_new_at(old, out, sg, i + 1, k) : out[k];
+            set_bit(k, delta_static_event(t[k], pm, pk));
+        }
+    }
+}
+
+// An accepted proposal: old[k0..n) becomes the new partial sums (whole block;
+// every thread calls it after a barrier that follows delta_walk).  U = the
+// positions each thread has in flight.
+template <int U>
+__device__ __forceinline__ void delta_commit(double *old, const double *out, int n, const DeltaSegs &sg, int tid,
+                                             int nthreads) {
+    const int nseg = sg.nseg, k0 = sg.k0;
+    if (nseg == 0 || k0 + tid >= n) return;
+    // the segment of this thread's first position (binary search), then forward
+    int lo = 0, hi = nseg - 1;
+    const int k1 = k0 + tid;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((sg.sm[mid] & kSegPosMask) <= k1) lo = mid;
+        else hi = mid - 1;
+    }
+    int i = lo;
+    int nxt = i + 1 < nseg ? (sg.sm[i + 1] & kSegPosMask) : INT_MAX;
+    for (int kb = k1; kb < n; kb += U * nthreads) {
+        double src[U], val[U];
+        int mode[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * nthreads;
+            while (k >= nxt) {
+                ++i;
+                nxt = i + 1 < nseg ? (sg.sm[i + 1] & kSegPosMask) : INT_MAX;
+            }
+            mode[u] = sg.sm[i] >> 29;
+            val[u] = sg.v[i];
+            const int kc = min(k, n - 1);
+            src[u] = mode[u] == kSegCopy ? out[kc] : old[kc];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = kb + u * nthreads;
+            if (k < n) old[k] = mode[u] == kSegOffset ? src[u] + val[u] : mode[u] == kSegValue ? val[u] : src[u];
+        }
+    }
 }
 
 }  // namespace tdstar

@@ -153,6 +153,8 @@ hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *pre
 hipError_t test_wave_delta_sum(const double *term, const double *old, const int *chg, int cnt, double C0,
                                double *prefix, double *C_end);
 hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast);
+hipError_t test_block_delta(const double *term, const double *term_old, double *old, const int *chg, int k0, int n,
+                            double *cprefix, double *C_end, long long *events, int *mask_ok);
 
 // ptS[i] = julia_sum_j w[j] * ((0.5*(z0[j]+z0[j+1])) / 1000) per ray (MCsub.jl:147-159).
 hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm = nullptr);

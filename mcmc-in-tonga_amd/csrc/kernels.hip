@@ -277,7 +277,59 @@ __global__ __launch_bounds__(64) void k_test_wave_delta_sum(const double *__rest
     if (threadIdx.x == 0) *C_end = C;
 }
 
+// The chain's chi^2 walk (exact_sum.h) on its own, as the chain uses it:
+// static event words of the OLD state kept across proposals, the changed terms
+// in their own words, the walk, the re-marking and the commit; then the kept
+// words are checked against words computed from scratch for the new state.
+__global__ __launch_bounds__(512) void k_test_block_delta(const double *__restrict__ term,
+                                                          const double *__restrict__ term_old, double *old,
+                                                          const int *__restrict__ chg, int k0, int n, double *cprefix,
+                                                          double *C_end, long long *events, int *mask_ok) {
+    __shared__ DeltaSegs sg;
+    __shared__ unsigned long long smask[1024], cmask[1024], check[1024];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int W = delta_words(n);
+    delta_marks(term_old, old, nullptr, n, smask, wv, W, 8, lane);
+    for (int w = wv; w < W; w += 8) {
+        const unsigned long long m = __ballot(64 * w + lane < n && chg[min(64 * w + lane, n - 1)] != 0);
+        if (lane == 0) cmask[w] = m;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const double C0 = k0 > 0 ? old[k0 - 1] : 0.0;
+        long long diag[4] = {0, 0, 0, 0};
+        double C = C0;
+        if (k0 < n) C = delta_walk(term, old, chg, k0, n, C0, smask, cmask, cprefix, sg, lane, diag);
+        else if (lane == 0) sg.nseg = 0;
+        const long long ev = diag[0] + diag[3];
+        if (lane == 0) {
+            *C_end = C;
+            *events = ev;
+        }
+        wave_sync_lds();
+        delta_remark(term, old, cprefix, n, sg, smask, lane);
+    }
+    __syncthreads();
+    delta_commit<4>(old, cprefix, n, sg, tid, 512);
+    __syncthreads();
+    delta_marks(term, old, nullptr, n, check, wv, W, 8, lane);
+    __syncthreads();
+    if (tid == 0) {
+        int ok = 1;
+        for (int w = 0; w < W; ++w) ok &= (check[w] == smask[w]) & (cmask[w] == 0ull);
+        *mask_ok = ok;
+    }
+}
+
 }  // namespace
+
+hipError_t test_block_delta(const double *term, const double *term_old, double *old, const int *chg, int k0, int n,
+                            double *cprefix, double *C_end, long long *events, int *mask_ok) {
+    if (n > 64 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_test_block_delta, dim3(1), dim3(512), 0, nullptr, term, term_old, old, chg, k0, n, cprefix,
+                       C_end, events, mask_ok);
+    return hipGetLastError();
+}
 
 hipError_t test_wave_delta_sum(const double *term, const double *old, const int *chg, int cnt, double C0,
                                double *prefix, double *C_end) {

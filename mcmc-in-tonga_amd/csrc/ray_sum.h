@@ -11,13 +11,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "wave_ops.h"
+
 namespace tdstar {
 
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <class Z>
 __device__ __forceinline__ double seg_term_z(const double *__restrict__ w, const Z &zeta, int k) {

@@ -9,6 +9,13 @@
 
 namespace tdstar {
 
+// LDS writes of this wave visible to its own later reads (no block barrier)
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---- cross-lane reductions on 64-bit keys through DPP (VALU, no LDS) ----
 // A non-negative double orders like its bit pattern, so distances reduce as
 // unsigned 64-bit keys.  update_dpp returns `old` in lanes whose source is out

@@ -32,13 +32,13 @@ def main():
     ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000, chain=1), tt.random_model(N, 3))
     ch.run(2000 if nrays == 0 else 200)
     L = tt.lib()
-    out0 = (ctypes.c_int64 * 72)()
+    out0 = (ctypes.c_int64 * 80)()
     L.tdt_chain_profile(ch.h, 1, out0)
     st0 = ch.stats()
     t0 = time.perf_counter()
     ch.run(iters)
     el = time.perf_counter() - t0
-    out = (ctypes.c_int64 * 72)()
+    out = (ctypes.c_int64 * 80)()
     L.tdt_chain_profile(ch.h, 0, out)
     cyc = np.array(out[:7], dtype=np.float64) - np.array(out0[:7], dtype=np.float64)
     cyc[6] += (out[12] - out0[12]) + (out[13] - out0[13])  # G = commit + next proposal + barrier
@@ -71,6 +71,8 @@ def main():
     res["chi2 scan rounds per proposal"] = round((out[65] - out0[65]) / ev, 2)
     res["per evaluated proposal: tiles hit, points seen, points changed, rays changed"] = [
         round((out[k] - out0[k]) / ev, 1) for k in (68, 69, 70, 71)]
+    res["chi2 walk (rays in HBM) per proposal: events, batch-load cycles, walk cycles, terms one by one"] = [
+        round((out[k] - out0[k]) / ev, 1) for k in (72, 73, 74, 75)]
     res["F wave 0: cycles to scan end / to decision (per iter)"] = [round((out[k] - out0[k]) / iters, 1)
                                                                      for k in (66, 67)]
     print(json.dumps(res, indent=1))

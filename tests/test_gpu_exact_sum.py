@@ -5,6 +5,7 @@ bit whenever they claim success, and claim success on realistic data (the
 one-wave sum always does).  Reference: a Python loop of IEEE-754 double adds
 (the same operation sequence as the Julia loop)."""
 import ctypes
+import itertools
 
 import numpy as np
 import pytest
@@ -186,3 +187,104 @@ def test_delta_sum_adversarial(tt):
     # every term changed / none changed
     delta_check(tt, base, base * 1.0000001, 50.0)
     delta_check(tt, base, base.copy(), 50.0)
+
+
+# ---- the chain's chi^2 walk (exact_sum.h delta_marks / delta_walk / delta_remark / delta_commit) ----
+def block_check(tt, old_terms, new_terms, k0=None):
+    """old/new terms over the whole ray list (C_{-1} = 0); they may differ only
+    from k0 on.  The walk must give the strictly sequential new partial sums."""
+    old_terms = np.ascontiguousarray(old_terms, dtype=np.float64)
+    new_terms = np.ascontiguousarray(new_terms, dtype=np.float64)
+    n = len(old_terms)
+    diff = (old_terms != new_terms) & ~(np.isnan(old_terms) & np.isnan(new_terms))
+    changed = diff.astype(np.int32)
+    if k0 is None:
+        k0 = int(np.argmax(diff)) if diff.any() else n
+    assert not diff[:k0].any()
+    old_prefix = np.array(list(itertools.accumulate(old_terms.tolist())), dtype=np.float64)
+    want = np.array(list(itertools.accumulate(new_terms.tolist())), dtype=np.float64)
+    pre = np.zeros(n)
+    ce = ctypes.c_double()
+    ev = ctypes.c_int64()
+    ok = ctypes.c_int32()
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    assert tt.lib().tdt_block_delta_sum(0, P(new_terms), P(old_terms), P(old_prefix),
+                                        changed.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), k0, n, P(pre),
+                                        ctypes.byref(ce), ctypes.byref(ev), ctypes.byref(ok)) == 0
+    assert ok.value == 1, "event words kept across the proposal differ from the new state's"
+    same = (pre == want) | (np.isnan(pre) & np.isnan(want))
+    bad = np.nonzero(~same)[0]
+    assert len(bad) == 0, (k0, bad[:5], pre[bad[:5]], want[bad[:5]])
+    end = want[-1] if k0 < n else (want[k0 - 1] if k0 > 0 else 0.0)
+    assert ce.value == end or (np.isnan(ce.value) and np.isnan(end)), (ce.value, end)
+    return ev.value
+
+
+def test_block_delta_chain_like(tt):
+    """The chain's case at the 381-ray and 10k-ray sizes: a few changed rays."""
+    rng = np.random.default_rng(31)
+    for trial in range(60):
+        n = int(rng.choice([1, 2, 63, 64, 65, 381, 1000, 4097, 10000]))
+        old = rng.exponential(float(rng.choice([1.0, 36.0, 1e-3])), n)
+        new = old.copy()
+        idx = rng.choice(n, size=min(n, int(rng.integers(1, 40))), replace=False)
+        new[idx] = old[idx] * rng.uniform(0.2, 3.0, len(idx))
+        ev = block_check(tt, old, new)
+        if n >= 1000:
+            assert ev < 200, ev  # O(events): the changed terms and a few binade changes
+
+
+def test_block_delta_adversarial(tt):
+    rng = np.random.default_rng(32)
+    base = rng.exponential(36.0, 3000)
+    # ties everywhere (odd and even offsets), against a large starting sum
+    ties = np.concatenate([[5000.0], (rng.integers(1, 9, 2999) * 2 + 1) * 2.0 ** -34])
+    for d in (2.0 ** -38, 3 * 2.0 ** -38, 1.0, -0.5, 1e-3):
+        new = ties.copy()
+        new[1] += d
+        block_check(tt, ties, new)
+    # the new sum crosses binades the old one does not (and back), offsets near powers of two
+    for k, v in ((3, 9000.0), (3, 0.0), (40, 1e-9), (2000, 7.5e4)):
+        new = base.copy()
+        new[k] = v
+        block_check(tt, base, new)
+    near = np.concatenate([[8191.0], np.full(500, 2.0 ** -10)])
+    new = near.copy()
+    new[0] = 8191.5
+    block_check(tt, near, new)
+    # huge relative changes, zeros, NaN / inf terms
+    for k, v in ((5, 1e12), (7, np.inf), (9, np.nan), (9, -1.0)):
+        new = base.copy()
+        new[k] = v
+        block_check(tt, base, new)
+    z = np.zeros(300)
+    new = z.copy()
+    new[100] = 5.0
+    block_check(tt, z, new)
+    # every term changed (dense events: the term-by-term path), none changed (empty tail)
+    block_check(tt, base, base * 1.0000001)
+    block_check(tt, base, base.copy())
+    # more events than the segment table holds (materialised into the copy buffer)
+    new = base.copy()
+    new[::7] *= 1.5
+    block_check(tt, base, new)
+    # tiny sums: binade changes at nearly every term
+    tiny = rng.exponential(1e-300, 2000)
+    new = tiny.copy()
+    new[10] *= 2
+    block_check(tt, tiny, new)
+    # a tail start k0 before the first changed term (the chain's k0 is the first changed ray)
+    new = base.copy()
+    new[1500] += 1.0
+    block_check(tt, base, new, k0=1000)
+    block_check(tt, base, base.copy(), k0=0)
+
+
+@pytest.mark.parametrize("n", [20000, 65536])
+def test_block_delta_long(tt, n):
+    rng = np.random.default_rng(n)
+    old = rng.exponential(1.3, n)
+    new = old.copy()
+    idx = rng.choice(n, size=16, replace=False)
+    new[idx] = rng.exponential(1.3, 16)
+    assert block_check(tt, old, new) < 200
