@@ -41,7 +41,6 @@ struct td_chain {
     ChainScalars *st_dev = nullptr;
     ChainScalars *st_host = nullptr;  // pinned
     NNWork nn;
-    std::vector<int> tile_start_host;
 };
 
 namespace {
@@ -172,6 +171,8 @@ T *carve(char *&cur, size_t count) {
 int device_setup(td_chain *ch) {
     td_ctx *c = ch->ctx;
     const int64_t P = c->g.P, n = c->g.n;
+    if (P >= (int64_t)1 << 26)  // tile_start packs start << 5 | count
+        return set_err(c, TD_ERR_ARG, "td_chain_create: more than 2^26 ray points");
     // ---- tiles: <= kTilePts consecutive points of one ray; bounding boxes
     //      rounded OUTWARD to FP32 (the lower bound stays valid, LDS holds them) ----
     std::vector<int> tstart, tray, pt_ray((size_t)P);
@@ -186,6 +187,8 @@ int device_setup(td_chain *ch) {
     const int ntiles = (int)tstart.size();
     tstart.push_back((int)P);
     std::vector<float> lo(3 * (size_t)ntiles), hi(3 * (size_t)ntiles);
+    std::vector<int> tcount((size_t)ntiles);
+    for (int t = 0; t < ntiles; ++t) tcount[(size_t)t] = tstart[(size_t)t + 1] - tstart[(size_t)t];
     for (int t = 0; t < ntiles; ++t) {
         double l[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, h[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
         for (int q = tstart[(size_t)t]; q < tstart[(size_t)t + 1]; ++q) {
@@ -204,7 +207,57 @@ int device_setup(td_chain *ch) {
             hi[(size_t)a * ntiles + t] = fh;
         }
     }
-    ch->tile_start_host = tstart;
+    // ---- tiles in a spatial order (Morton code of the box centre) so that 16
+    //      consecutive tiles form a compact SUPER-TILE; its box is the union of
+    //      theirs.  Rays in HBM test super-tiles first (chain_kernels.hip phase B).
+    //      A tile's points: tile_sc[t] = start << 5 | count ----
+    std::vector<int> torder((size_t)ntiles);
+    {
+        double gl[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, gh[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+        for (int t = 0; t < ntiles; ++t)
+            for (int a = 0; a < 3; ++a) {
+                gl[a] = std::min(gl[a], (double)lo[(size_t)a * ntiles + t]);
+                gh[a] = std::max(gh[a], (double)hi[(size_t)a * ntiles + t]);
+            }
+        std::vector<uint64_t> key((size_t)ntiles);
+        for (int t = 0; t < ntiles; ++t) {
+            uint64_t k = 0;
+            uint32_t c3[3];
+            for (int a = 0; a < 3; ++a) {
+                const double ctr = 0.5 * ((double)lo[(size_t)a * ntiles + t] + (double)hi[(size_t)a * ntiles + t]);
+                const double u = gh[a] > gl[a] ? (ctr - gl[a]) / (gh[a] - gl[a]) : 0.0;
+                c3[a] = (uint32_t)std::min(1023.0, std::max(0.0, std::floor(u * 1024.0)));
+            }
+            for (int bit = 9; bit >= 0; --bit)
+                for (int a = 0; a < 3; ++a) k = (k << 1) | ((c3[a] >> bit) & 1u);
+            key[(size_t)t] = k;
+            torder[(size_t)t] = t;
+        }
+        std::stable_sort(torder.begin(), torder.end(), [&](int a, int b) { return key[(size_t)a] < key[(size_t)b]; });
+    }
+    std::vector<int> tsc((size_t)ntiles + 1, 0), tray2((size_t)ntiles);
+    std::vector<float> lo2(lo.size()), hi2(hi.size());
+    for (int i = 0; i < ntiles; ++i) {
+        const int t = torder[(size_t)i];
+        tsc[(size_t)i] = (tstart[(size_t)t] << 5) | tcount[(size_t)t];
+        tray2[(size_t)i] = tray[(size_t)t];
+        for (int a = 0; a < 3; ++a) {
+            lo2[(size_t)a * ntiles + i] = lo[(size_t)a * ntiles + t];
+            hi2[(size_t)a * ntiles + i] = hi[(size_t)a * ntiles + t];
+        }
+    }
+    const int nsuper = (ntiles + kTilePts - 1) / kTilePts;
+    std::vector<float> slo(3 * (size_t)std::max(nsuper, 1)), shi(3 * (size_t)std::max(nsuper, 1));
+    for (int S = 0; S < nsuper; ++S)
+        for (int a = 0; a < 3; ++a) {
+            float l = HUGE_VALF, h = -HUGE_VALF;
+            for (int i = S * kTilePts; i < std::min(ntiles, (S + 1) * kTilePts); ++i) {
+                l = std::min(l, lo2[(size_t)a * ntiles + i]);
+                h = std::max(h, hi2[(size_t)a * ntiles + i]);
+            }
+            slo[(size_t)a * nsuper + S] = l;
+            shi[(size_t)a * nsuper + S] = h;
+        }
     const int cap = std::max<int>(ch->prm.max_cells, (int)ch->x.size()) + 1;
     // ---- bucket grid over the cells: ~2 cells per bucket at the starting size ----
     const double glo[3] = {ch->P.xmin, ch->P.ymin, ch->P.zmin}, ghi[3] = {ch->P.xmax, ch->P.ymax, ch->P.zmax};
@@ -226,6 +279,7 @@ int device_setup(td_chain *ch) {
     const size_t Pn = (size_t)std::max<int64_t>(P, 1), nn = (size_t)std::max<int64_t>(n, 1);
     add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * Pn);
     add(sizeof(float) * 3 * ntiles); add(sizeof(float) * 3 * ntiles); add(sizeof(double) * (ntiles + 1)); add(sizeof(double) * (ntiles + 1));
+    add(sizeof(float) * 3 * std::max(nsuper, 1)); add(sizeof(float) * 3 * std::max(nsuper, 1));
     add(sizeof(double) * 4 * cap); add(sizeof(double) * (cap + 2)); for (int i = 0; i < 4; ++i) add(sizeof(int) * cap);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn); add(Pn);
@@ -253,6 +307,9 @@ int device_setup(td_chain *ch) {
     d.tile_maxd = carve<double>(cur, ntiles + 1);
     d.tile_cmax = carve<double>(cur, ntiles + 1);
     d.ntiles = ntiles;
+    float *slo_d = carve<float>(cur, 3 * (size_t)std::max(nsuper, 1));
+    float *shi_d = carve<float>(cur, 3 * (size_t)std::max(nsuper, 1));
+    d.super_lo = slo_d; d.super_hi = shi_d; d.nsuper = nsuper;
     double *cells = carve<double>(cur, 4 * (size_t)cap);
     d.cx = cells; d.cy = cells + cap; d.cz = cells + 2 * cap; d.czeta = cells + 3 * cap;
     double *logN_d = carve<double>(cur, (size_t)cap + 2);
@@ -301,11 +358,13 @@ int device_setup(td_chain *ch) {
     for (size_t k = 0; k < logN.size(); ++k) logN[k] = tdchain::det_log((double)k);
     struct Up { void *d; const void *h; size_t b; } ups[] = {
         {logN_d, logN.data(), sizeof(double) * logN.size()},
-        {tile_start, tstart.data(), sizeof(int) * tstart.size()},
-        {tile_ray_d, tray.data(), sizeof(int) * tray.size()},
+        {tile_start, tsc.data(), sizeof(int) * tsc.size()},
+        {tile_ray_d, tray2.data(), sizeof(int) * tray2.size()},
         {pt_ray_d, pt_ray.data(), sizeof(int) * (size_t)P},
-        {tlo, lo.data(), sizeof(float) * lo.size()},
-        {thi, hi.data(), sizeof(float) * hi.size()},
+        {tlo, lo2.data(), sizeof(float) * lo2.size()},
+        {thi, hi2.data(), sizeof(float) * hi2.size()},
+        {slo_d, slo.data(), sizeof(float) * slo.size()},
+        {shi_d, shi.data(), sizeof(float) * shi.size()},
         {cells, hc.data(), sizeof(double) * hc.size()},
         {d.order, ident.data(), sizeof(int) * (size_t)cap},
         {d.rank, rank0.data(), sizeof(int) * (size_t)cap},

@@ -55,12 +55,15 @@ struct DevChain {
     const int *ray_off, *pt_ray;
     int P, n;
     // tiles of <= kTilePts consecutive points of one ray
-    const int *tile_start;            // [ntiles+1]
+    // tiles in a spatial (Morton) order; super-tile S = tiles [16 S, 16 S + 16)
+    const int *tile_start;            // [ntiles] start << 5 | count of the tile's points
     const int *tile_ray;              // [ntiles] ray of each tile
     const float *tile_lo, *tile_hi;   // [3][ntiles] SoA, outward-rounded to FP32
     double *tile_maxd;                // [ntiles] max cached distance of the tile's points
     double *tile_cmax;                // [ntiles] scratch: hit tiles' maxima if accepted
     int ntiles;
+    const float *super_lo, *super_hi;  // [3][nsuper] union of the member tiles' boxes
+    int nsuper;
     // cells by slot
     double *cx, *cy, *cz, *czeta;  // [cap]
     const double *logN;            // [cap+2] det_log(k), the MH model-size factor

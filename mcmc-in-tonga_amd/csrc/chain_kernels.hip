@@ -118,6 +118,7 @@ struct Shared {
     double phi_n;
     int accept;
     int n_tiles, n_changed, n_orphans, n_rays, k0;
+    int n_super[2];  // rays in HBM: super-tiles hit, by iteration parity (the next iteration refreshes their maxima)
     int pts_seen, ray_pts;
     // bucket-grid update of an accepted proposal (applied by the last wave in phase G)
     int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site
@@ -155,9 +156,12 @@ struct Shared {
 
 // LDS carve-up (host and device agree on it through this function).
 struct LdsPlan {
-    size_t scratch, draws, smask, cmask, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
+    size_t scratch, draws, smask, cmask, slo, shi, smax, shit, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
         tS, sig, rflag, rhit, ord, total;
+    bool super_lds;  // rays in HBM: super-tile boxes, maxima and hit lists in LDS
 };
+
+constexpr size_t kLdsBudget = 160 * 1024;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -189,6 +193,15 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
     } else {  // the chi^2 walk's event words (exact_sum.h): static ones, kept; changed rays
         L.smask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
         L.cmask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
+        // super-tiles (16 tiles each): boxes, maxima, two hit lists
+        const int ns = (ntiles + kTilePts - 1) / kTilePts;
+        size_t q = o;
+        L.slo = q; q += align16(sizeof(float) * 3 * ns);
+        L.shi = q; q += align16(sizeof(float) * 3 * ns);
+        L.smax = q; q += align16(sizeof(double) * ns);
+        L.shit = q; q += align16(sizeof(int) * 2 * ns);
+        L.super_lds = q <= kLdsBudget;
+        if (L.super_lds) o = q;
     }
     L.total = o;
     return L;
@@ -541,9 +554,26 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     __syncthreads();
     unsigned long long *smask = reinterpret_cast<unsigned long long *>(lds + L.smask);
     unsigned long long *cmask = reinterpret_cast<unsigned long long *>(lds + L.cmask);
+    const int NS = d.nsuper;
+    float *slo = reinterpret_cast<float *>(lds + L.slo), *shi = reinterpret_cast<float *>(lds + L.shi);
+    double *smax = reinterpret_cast<double *>(lds + L.smax);
+    int *shit = reinterpret_cast<int *>(lds + L.shit);
+    const bool super_on = !SMALL && L.super_lds;
     if constexpr (!SMALL) {  // rays in HBM: the chi^2 walk's static event words of the current state
         delta_marks(v.term, v.prefix, nullptr, n, smask, wv, delta_words(n), kWaves, lane);
         for (int w = tid; w < delta_words(n); w += kChainThreads) cmask[w] = 0ull;
+        if (super_on) {  // super-tile boxes, and maxima = the max of their tiles' maxima
+            for (int i = tid; i < 3 * NS; i += kChainThreads) {
+                slo[i] = d.super_lo[i];
+                shi[i] = d.super_hi[i];
+            }
+            for (int S = tid; S < NS; S += kChainThreads) {
+                double m = 0.0;
+                for (int t = S * kTilePts; t < min(NT, (S + 1) * kTilePts); ++t) m = fmax(m, d.tile_maxd[t]);
+                smax[S] = m;
+            }
+            if (tid == 0) sh.n_super[0] = sh.n_super[1] = 0;
+        }
         __syncthreads();
     }
 
@@ -570,7 +600,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const long long iter0 = sh.iter;
     double phi_r = sh.phi;
     int cur_r = 0;
-    bool pend_r = false;  // rays in HBM: an accepted proposal's chi^2 partial sums not yet written
+    bool pend_r = false;    // rays in HBM: an accepted proposal's chi^2 partial sums not yet written
+    bool pend_sup = false;  // rays in HBM: its super-tiles' maxima not yet refreshed
     for (long long it = 0; it < iters; ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
         if constexpr (!SMALL) {
@@ -578,6 +609,17 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             // after at least one barrier): off its critical path, before this one's tiles
             if (pend_r) delta_commit<16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
             pend_r = false;
+            if (pend_sup) {  // its hit super-tiles: max of their tiles' new maxima (a tile row each)
+                const int par = (int)((it - 1) & 1), nsh = sh.n_super[par];
+                for (int i = tid >> 4; i < nsh; i += kChainThreads / kTilePts) {
+                    const int S = shit[par * NS + i], t = S * kTilePts + (tid & 15);
+                    unsigned long long mk = t < NT ? (unsigned long long)__double_as_longlong(d.tile_maxd[t]) : 0ull;
+                    mk = row_max_u64(mk);
+                    if ((tid & 15) == 15) smax[S] = __longlong_as_double((long long)mk);
+                }
+                __syncthreads();
+                pend_sup = false;
+            }
         }
         bool acc_r = false;
         const PState &cur = sh.ps[sh.cur];
@@ -603,7 +645,47 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 const int nthr = query ? kChainThreads - 64 : kChainThreads;
                 // tiles in flight per thread: LDS latency is short; HBM needs more
                 constexpr int TU = SMALL ? 3 : 8;
-                if (tid < nthr)
+                if (super_on) {
+                    // rays in HBM: the super-tiles (LDS) first, then the tiles of those hit
+                    const int par = (int)(it & 1);
+                    int *hl = shit + par * NS;
+                    if (tid < nthr)
+                        for (int S0 = tid; S0 < NS; S0 += 4 * nthr) {
+                            bool hit[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int S = min(S0 + u * nthr, NS - 1);
+                                const float thr = tile_thr(smax[S]);
+                                const bool h0 = tile_may_hit(slo, shi, NS, S, tq0, thr);
+                                const bool h1 = tile_may_hit(slo, shi, NS, S, tq1, thr);
+                                hit[u] = S0 + u * nthr < NS && ((q0 && h0) || (q1 && h1));
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                if (hit[u]) hl[atomicAdd(&sh.n_super[par], 1)] = S0 + u * nthr;
+                        }
+                    __syncthreads();  // (the query wave too: it starts its query after this)
+                    const int nitems = sh.n_super[par] * kTilePts;
+                    if (tid < nthr)
+                        for (int i0 = tid; i0 < nitems; i0 += 4 * nthr) {
+                            bool hit[4];
+                            int tt[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int i = min(i0 + u * nthr, nitems - 1);
+                                const int t = min(hl[i >> 4] * kTilePts + (i & 15), NT - 1);
+                                const float thr = tile_thr(v.tmaxd[t]);
+                                const bool h0 = tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr);
+                                const bool h1 = tile_may_hit(v.tlo, v.thi, NT, t, tq1, thr);
+                                tt[u] = t;
+                                hit[u] = i0 + u * nthr < nitems && hl[i >> 4] * kTilePts + (i & 15) < NT &&
+                                         ((q0 && h0) || (q1 && h1));
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                if (hit[u]) v.thit[atomicAdd(&sh.n_tiles, 1)] = tt[u];
+                        }
+                } else if (tid < nthr)
                     for (int t0 = tid; t0 < NT; t0 += TU * nthr) {
                         bool hit[TU];
 #pragma unroll
@@ -647,8 +729,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 int seen = 0;
                 for (int item = tid; item < nt * kTilePts; item += kChainThreads) {
                     const int t = v.thit[item / kTilePts];
-                    const int q = v.tstart[t] + item % kTilePts;
-                    if (q >= v.tstart[t + 1]) continue;
+                    const int sc = v.tstart[t];  // start << 5 | count
+                    if (item % kTilePts >= (sc & 31)) continue;
+                    const int q = (sc >> 5) + item % kTilePts;
                     ++seen;
                     const int ray = v.tray[t];
                     // independent loads: one round trip
@@ -796,7 +879,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
                     // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
                     atomicAdd((unsigned long long *)&sh.bytes,
-                              (unsigned long long)((long long)NT * 32 + (long long)sh.pts_seen * 36 +
+                              (unsigned long long)((super_on ? (long long)NS * 32 +
+                                                                  (long long)sh.n_super[it & 1] * kTilePts * 32
+                                                             : (long long)NT * 32) +
+                                                   (long long)sh.pts_seen * 36 +
                                                    (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
                                                    (long long)sh.ray_pts * 17 + (long long)(n - sh.k0) * 28));
                 }
@@ -826,9 +912,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 const int nt = sh.n_tiles;
                 for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 256) {
                     const int t = v.thit[i / kTilePts];
-                    const int q = v.tstart[t] + (i % kTilePts);
+                    const int sc = v.tstart[t];  // start << 5 | count
+                    const int q = (sc >> 5) + (i % kTilePts);
                     unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
-                    if (q < v.tstart[t + 1]) {
+                    if (i % kTilePts < (sc & 31)) {
                         const double cd = d.cand_d[q], bd = d.best_d[q];
                         mk = (unsigned long long)__double_as_longlong(d.cand_flag[q] ? cd : bd);
                     }
@@ -851,8 +938,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     d.zeta0[q] = d.cand_z[q];
                     d.cand_flag[q] = 0;
                 }
-                if (fwd && action != tdchain::kChange)
+                if (fwd && action != tdchain::kChange) {
                     for (int i = tid; i < nt; i += kChainThreads) v.tmaxd[v.thit[i]] = v.ctm[i];
+                    pend_sup = super_on;  // their super-tiles' maxima: at the top of the next iteration
+                }
                 for (int rr = tid; rr < nr; rr += kChainThreads) {
                     const int r = v.rhit[rr];
                     v.ptS[r] = v.cptS[r];
@@ -951,6 +1040,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.spec_ok = 0;
                     sh.early_reject = 0;
                     sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
+                    sh.n_super[(it + 1) & 1] = 0;  // the other parity's list is refreshed first
                     sh.pts_seen = sh.ray_pts = 0;
                     sh.k0 = n;
                     sh.accept = 0;
@@ -1021,11 +1111,10 @@ __global__ void k_tile_max(const int *__restrict__ tile_start, int ntiles, const
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
     double mx = -1.0;
-    for (int q = tile_start[t]; q < tile_start[t + 1]; ++q) mx = fmax(mx, best_d[q]);
+    const int sc = tile_start[t];  // start << 5 | count
+    for (int q = sc >> 5; q < (sc >> 5) + (sc & 31); ++q) mx = fmax(mx, best_d[q]);
     tile_maxd[t] = mx;
 }
-
-constexpr size_t kLdsBudget = 160 * 1024;
 
 }  // namespace
 
