@@ -38,6 +38,10 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
  * [56 + w] phase F of wave w, [64] chi^2 tail terms, [65] chi^2 scan rounds.
  * Never enabled in measured runs. */
 int tdt_chain_profile(td_chain *ch, int enable, int64_t out[80]);
+/* LDS plan of a device chain: [0] bytes of the LDS layout (tiles, rays and
+ * order mirrored), [1] bytes of the HBM layout, [2] 1 if the HBM layout holds
+ * its super-tiles in LDS, [3] 1 if runs take the LDS layout. */
+int tdt_chain_lds(td_chain *ch, int64_t out[4]);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);

@@ -78,6 +78,7 @@ SIGNATURES = {
     "tdt_draws": (None, [_u64, _u32, _u64, _pd]),
     "tdt_propose": (ctypes.c_int, [ctypes.POINTER(TdChainParams), _u64, _i64, _pd, _pd, _pd, _pd, _d, _pd]),
     "tdt_chain_profile": (ctypes.c_int, [_vp, ctypes.c_int, _pi64]),
+    "tdt_chain_lds": (ctypes.c_int, [_vp, _pi64]),
     "tdt_set_nn_method": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_chain_set_lds_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_exact_sum": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _d, _pd, _pd, _pi32]),

@@ -643,6 +643,12 @@ int tdt_chain_set_lds_mode(td_chain *ch, int mode) {
     return TD_OK;
 }
 
+int tdt_chain_lds(td_chain *ch, int64_t out[4]) {
+    if (!ch || ch->engine != TD_ENGINE_DEVICE || !out) return TD_ERR_ARG;
+    chain_lds_sizes(ch->dev, out);
+    return TD_OK;
+}
+
 int tdt_chain_profile(td_chain *ch, int enable, int64_t out[80]) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE) return TD_ERR_ARG;
     ch->dev.profile = enable;

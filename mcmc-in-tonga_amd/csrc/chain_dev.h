@@ -101,5 +101,7 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
 // (workgroup b runs chain b).  `host` = the descriptors, `dev` = their device
 // copy, contiguous (the kernel reads its fields from global memory).
 hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s);
+// LDS bytes of the two layouts, whether super-tiles fit, and the layout chain_run takes.
+void chain_lds_sizes(const DevChain &d, int64_t out[4]);
 
 }  // namespace tdstar

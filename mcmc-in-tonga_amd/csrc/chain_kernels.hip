@@ -46,6 +46,7 @@ using tdchain::Proposal;
 constexpr int kWaves = kChainThreads / 64;
 static_assert(kTilePts == 16, "a tile is one 16-lane DPP row (row_max_u64)");
 constexpr int kOrphanLds = 256; // orphan records kept in LDS (more: read back from HBM)
+constexpr int kListLds = 1024;  // rays in HBM: hit tiles / changed rays / hit super-tiles kept in LDS
 
 // A point whose nearest cell is removed or moved: re-searched in phase D.
 struct OrphanRec {
@@ -156,9 +157,10 @@ struct Shared {
 
 // LDS carve-up (host and device agree on it through this function).
 struct LdsPlan {
-    size_t scratch, draws, smask, cmask, slo, shi, smax, shit, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
+    size_t scratch, draws, smask, cmask, slo, shi, smax, shit, hrec, rhitl, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
         tS, sig, rflag, rhit, ord, total;
     bool super_lds;  // rays in HBM: super-tile boxes, maxima and hit lists in LDS
+    bool lists_lds;  // rays in HBM: the first kListLds hit tiles (as records) and changed rays in LDS
 };
 
 constexpr size_t kLdsBudget = 160 * 1024;
@@ -193,13 +195,19 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
     } else {  // the chi^2 walk's event words (exact_sum.h): static ones, kept; changed rays
         L.smask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
         L.cmask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
-        // super-tiles (16 tiles each): boxes, maxima, two hit lists
-        const int ns = (ntiles + kTilePts - 1) / kTilePts;
+        // the first hit tiles as {tile, start << 5 | count, ray} records, the first changed rays
         size_t q = o;
+        L.hrec = q; q += align16(sizeof(int4) * kListLds);
+        L.rhitl = q; q += align16(sizeof(int) * kListLds);
+        L.lists_lds = q <= kLdsBudget;
+        if (L.lists_lds) o = q;
+        // super-tiles (16 tiles each): boxes, maxima (FP32, rounded up), two hit lists
+        const int ns = (ntiles + kTilePts - 1) / kTilePts;
+        q = o;
         L.slo = q; q += align16(sizeof(float) * 3 * ns);
         L.shi = q; q += align16(sizeof(float) * 3 * ns);
-        L.smax = q; q += align16(sizeof(double) * ns);
-        L.shit = q; q += align16(sizeof(int) * 2 * ns);
+        L.smax = q; q += align16(sizeof(float) * ns);
+        L.shit = q; q += align16(sizeof(int) * 2 * kListLds);
         L.super_lds = q <= kLdsBudget;
         if (L.super_lds) o = q;
     }
@@ -214,6 +222,23 @@ struct Views {
     const double *tS, *sig;
     const int *tstart, *ray_off, *tray;
     int *thit, *rflag, *rhit, *ord;
+    // rays in HBM: the first kListLds changed rays in LDS (rhit), the rest in rhit_g;
+    // the first kListLds hit tiles also as LDS records
+    int *rhit_g;
+    int rhit_cap;
+    int4 *hrec;
+    int hrec_cap;
+    __device__ __forceinline__ int ray_at(int i) const { return i < rhit_cap ? rhit[i] : rhit_g[i]; }
+    __device__ __forceinline__ void ray_put(int i, int r) const {
+        if (i < rhit_cap) rhit[i] = r;
+        else rhit_g[i] = r;
+    }
+    // hit tile i: {tile, start << 5 | count, ray}
+    __device__ __forceinline__ int4 tile_rec(int i) const {
+        if (i < hrec_cap) return hrec[i];
+        const int t = thit[i];
+        return int4{t, tstart[t], tray[t], 0};
+    }
 };
 
 // Result of one nearest-cell query, the same in every lane of the wave.
@@ -427,7 +452,7 @@ __device__ __forceinline__ void mark(const DevChain &d, const Views &v, Shared &
     d.cand_flag[p] = 1;
     d.changed[atomicAdd(&sh.n_changed, 1)] = p;
     if (atomicExch(&v.rflag[r], 1) == 0) {
-        v.rhit[atomicAdd(&sh.n_rays, 1)] = r;
+        v.ray_put(atomicAdd(&sh.n_rays, 1), r);
         atomicMin(&sh.k0, r);
     }
 }
@@ -466,6 +491,11 @@ __device__ __forceinline__ bool tile_may_hit(const float *lo, const float *hi, i
     return s * (1.0f - 0x1p-20f) <= thr;
 }
 __device__ __forceinline__ float tile_thr(double mx) { return (float)mx * (1.0f + 0x1p-20f); }
+// x rounded up to FP32 (x >= 0; the super-tile maxima)
+__device__ __forceinline__ float f32_up(double x) {
+    const float f = (float)x;
+    return (double)f < x ? __int_as_float(__float_as_int(f) + 1) : f;  // f >= 0 finite: the next float up
+}
 
 template <bool SMALL>
 __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters) {
@@ -485,6 +515,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     v.tlo = d.tile_lo; v.thi = d.tile_hi; v.tmaxd = d.tile_maxd; v.tstart = d.tile_start; v.thit = d.tiles_hit;
     v.ray_off = d.ray_off; v.ptS = d.ptS; v.prefix = d.prefix; v.cptS = d.cand_ptS; v.cprefix = d.cand_prefix;
     v.tS = d.tS; v.sig = d.sig; v.rflag = d.ray_flag; v.rhit = d.rays_hit; v.ord = d.order; v.tray = d.tile_ray;
+    v.rhit_g = d.rays_hit;
+    v.rhit_cap = 0;
+    v.hrec = nullptr;
+    v.hrec_cap = 0;
+    if (!SMALL && L.lists_lds) {
+        v.rhit = reinterpret_cast<int *>(lds + L.rhitl);
+        v.rhit_cap = kListLds;
+        v.hrec = reinterpret_cast<int4 *>(lds + L.hrec);
+        v.hrec_cap = kListLds;
+    }
     v.term = d.term;
     v.cterm = d.cand_term;
     v.ctm = d.tile_cmax;
@@ -522,6 +562,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         v.thit = reinterpret_cast<int *>(lds + L.thit);
         v.ctm = reinterpret_cast<double *>(lds + L.ctm);
         v.rhit = reinterpret_cast<int *>(lds + L.rhit);
+        v.rhit_cap = n;
         __syncthreads();  // ptS, tS, sig mirrored
     }
     // chi^2 term of every ray in the current state (MCsub.jl:171), cached: a
@@ -556,7 +597,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     unsigned long long *cmask = reinterpret_cast<unsigned long long *>(lds + L.cmask);
     const int NS = d.nsuper;
     float *slo = reinterpret_cast<float *>(lds + L.slo), *shi = reinterpret_cast<float *>(lds + L.shi);
-    double *smax = reinterpret_cast<double *>(lds + L.smax);
+    float *smax = reinterpret_cast<float *>(lds + L.smax);  // >= the max of its tiles' maxima
     int *shit = reinterpret_cast<int *>(lds + L.shit);
     const bool super_on = !SMALL && L.super_lds;
     if constexpr (!SMALL) {  // rays in HBM: the chi^2 walk's static event words of the current state
@@ -570,7 +611,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             for (int S = tid; S < NS; S += kChainThreads) {
                 double m = 0.0;
                 for (int t = S * kTilePts; t < min(NT, (S + 1) * kTilePts); ++t) m = fmax(m, d.tile_maxd[t]);
-                smax[S] = m;
+                smax[S] = f32_up(m);
             }
             if (tid == 0) sh.n_super[0] = sh.n_super[1] = 0;
         }
@@ -611,11 +652,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             pend_r = false;
             if (pend_sup) {  // its hit super-tiles: max of their tiles' new maxima (a tile row each)
                 const int par = (int)((it - 1) & 1), nsh = sh.n_super[par];
-                for (int i = tid >> 4; i < nsh; i += kChainThreads / kTilePts) {
-                    const int S = shit[par * NS + i], t = S * kTilePts + (tid & 15);
+                const bool all = nsh > kListLds;  // the list overflowed: every super-tile
+                for (int i = tid >> 4; i < (all ? NS : nsh); i += kChainThreads / kTilePts) {
+                    const int S = all ? i : shit[par * kListLds + i], t = S * kTilePts + (tid & 15);
                     unsigned long long mk = t < NT ? (unsigned long long)__double_as_longlong(d.tile_maxd[t]) : 0ull;
                     mk = row_max_u64(mk);
-                    if ((tid & 15) == 15) smax[S] = __longlong_as_double((long long)mk);
+                    if ((tid & 15) == 15) smax[S] = f32_up(__longlong_as_double((long long)mk));
                 }
                 __syncthreads();
                 pend_sup = false;
@@ -648,42 +690,51 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 if (super_on) {
                     // rays in HBM: the super-tiles (LDS) first, then the tiles of those hit
                     const int par = (int)(it & 1);
-                    int *hl = shit + par * NS;
+                    int *hl = shit + par * kListLds;
                     if (tid < nthr)
                         for (int S0 = tid; S0 < NS; S0 += 4 * nthr) {
                             bool hit[4];
 #pragma unroll
                             for (int u = 0; u < 4; ++u) {
                                 const int S = min(S0 + u * nthr, NS - 1);
-                                const float thr = tile_thr(smax[S]);
+                                const float thr = smax[S] * (1.0f + 0x1p-20f);
                                 const bool h0 = tile_may_hit(slo, shi, NS, S, tq0, thr);
                                 const bool h1 = tile_may_hit(slo, shi, NS, S, tq1, thr);
                                 hit[u] = S0 + u * nthr < NS && ((q0 && h0) || (q1 && h1));
                             }
 #pragma unroll
                             for (int u = 0; u < 4; ++u)
-                                if (hit[u]) hl[atomicAdd(&sh.n_super[par], 1)] = S0 + u * nthr;
+                                if (hit[u]) {
+                                    const int k = atomicAdd(&sh.n_super[par], 1);
+                                    if (k < kListLds) hl[k] = S0 + u * nthr;
+                                }
                         }
                     __syncthreads();  // (the query wave too: it starts its query after this)
-                    const int nitems = sh.n_super[par] * kTilePts;
+                    const int nsh = sh.n_super[par];
+                    const bool all = nsh > kListLds;  // the list overflowed: every tile
+                    const int nitems = all ? NS * kTilePts : nsh * kTilePts;
                     if (tid < nthr)
                         for (int i0 = tid; i0 < nitems; i0 += 4 * nthr) {
                             bool hit[4];
-                            int tt[4];
+                            int4 rec[4];
 #pragma unroll
                             for (int u = 0; u < 4; ++u) {
                                 const int i = min(i0 + u * nthr, nitems - 1);
-                                const int t = min(hl[i >> 4] * kTilePts + (i & 15), NT - 1);
+                                const int tu = (all ? (i >> 4) : hl[i >> 4]) * kTilePts + (i & 15);
+                                const int t = min(tu, NT - 1);
                                 const float thr = tile_thr(v.tmaxd[t]);
                                 const bool h0 = tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr);
                                 const bool h1 = tile_may_hit(v.tlo, v.thi, NT, t, tq1, thr);
-                                tt[u] = t;
-                                hit[u] = i0 + u * nthr < nitems && hl[i >> 4] * kTilePts + (i & 15) < NT &&
-                                         ((q0 && h0) || (q1 && h1));
+                                rec[u] = int4{t, v.tstart[t], v.tray[t], 0};  // loaded with the box
+                                hit[u] = i0 + u * nthr < nitems && tu < NT && ((q0 && h0) || (q1 && h1));
                             }
 #pragma unroll
                             for (int u = 0; u < 4; ++u)
-                                if (hit[u]) v.thit[atomicAdd(&sh.n_tiles, 1)] = tt[u];
+                                if (hit[u]) {
+                                    const int k = atomicAdd(&sh.n_tiles, 1);
+                                    v.thit[k] = rec[u].x;
+                                    if (k < v.hrec_cap) v.hrec[k] = rec[u];
+                                }
                         }
                 } else if (tid < nthr)
                     for (int t0 = tid; t0 < NT; t0 += TU * nthr) {
@@ -698,7 +749,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         }
 #pragma unroll
                         for (int u = 0; u < TU; ++u)
-                            if (hit[u]) v.thit[atomicAdd(&sh.n_tiles, 1)] = t0 + u * nthr;
+                            if (hit[u]) {
+                                const int k = atomicAdd(&sh.n_tiles, 1), t = t0 + u * nthr;
+                                v.thit[k] = t;
+                                if (!SMALL && k < v.hrec_cap) v.hrec[k] = int4{t, v.tstart[t], v.tray[t], 0};
+                            }
                     }
             }
             if (action == tdchain::kDeath)  // deleteat! shift, staged before we know if it is accepted
@@ -727,17 +782,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 const int rank_k = slot_k >= 0 ? d.rank[slot_k] : 0;
                 const double zeta_k = slot_k >= 0 ? d.czeta[slot_k] : 0.0;
                 int seen = 0;
-                for (int item = tid; item < nt * kTilePts; item += kChainThreads) {
-                    const int t = v.thit[item / kTilePts];
-                    const int sc = v.tstart[t];  // start << 5 | count
-                    if (item % kTilePts >= (sc & 31)) continue;
-                    const int q = (sc >> 5) + item % kTilePts;
-                    ++seen;
-                    const int ray = v.tray[t];
-                    // independent loads: one round trip
-                    const int s = d.best_s[q];
-                    const double bd = d.best_d[q];
-                    const double qx = d.px[q], qy = d.py[q], qz = d.pz[q];
+                // one candidate point: captured (birth, move), re-valued (change) or orphaned
+                // (death, move: its nearest cell is the selected one)
+                auto point = [&](int q, int ray, int s, double bd, double qx, double qy, double qz) {
                     if (action == tdchain::kBirth) {  // appended cell: strict capture
                         const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
                         if (dd < bd) mark(d, v, sh, q, ray, new_slot, dd, pp.zeta);
@@ -751,6 +798,47 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
                         if (dd < bd || (dd == bd && s >= 0 && rank_k < d.rank[s]))
                             mark(d, v, sh, q, ray, slot_k, dd, zeta_k);
+                    }
+                };
+                if constexpr (SMALL) {
+                    for (int item = tid; item < nt * kTilePts; item += kChainThreads) {
+                        const int t = v.thit[item / kTilePts];
+                        const int sc = v.tstart[t];  // start << 5 | count
+                        if (item % kTilePts >= (sc & 31)) continue;
+                        const int q = (sc >> 5) + item % kTilePts;
+                        ++seen;
+                        // independent loads: one round trip
+                        const int s = d.best_s[q];
+                        const double bd = d.best_d[q];
+                        const double qx = d.px[q], qy = d.py[q], qz = d.pz[q];
+                        point(q, v.tray[t], s, bd, qx, qy, qz);
+                    }
+                } else {
+                    constexpr int CU = 4;  // items in flight per thread (rays in HBM: latency)
+                    for (int item0 = tid; item0 < nt * kTilePts; item0 += CU * kChainThreads) {
+                        int qq[CU], rr[CU], ss[CU];
+                        double bb[CU], xx[CU], yy[CU], zz[CU];
+#pragma unroll
+                        for (int u = 0; u < CU; ++u) {  // every load of the CU items: one round trip
+                            const int item = item0 + u * kChainThreads;
+                            const int4 rec = v.tile_rec(min(item, nt * kTilePts - 1) / kTilePts);
+                            const int sc = rec.y;  // start << 5 | count
+                            const bool in = item < nt * kTilePts && item % kTilePts < (sc & 31);
+                            const int q = in ? (sc >> 5) + item % kTilePts : 0;
+                            qq[u] = in ? q : -1;
+                            rr[u] = rec.z;
+                            ss[u] = d.best_s[q];
+                            bb[u] = d.best_d[q];
+                            xx[u] = d.px[q];
+                            yy[u] = d.py[q];
+                            zz[u] = d.pz[q];
+                        }
+#pragma unroll
+                        for (int u = 0; u < CU; ++u)
+                            if (qq[u] >= 0) {
+                                ++seen;
+                                point(qq[u], rr[u], ss[u], bb[u], xx[u], yy[u], zz[u]);
+                            }
                     }
                 }
                 if (seen) atomicAdd(&sh.pts_seen, seen);
@@ -785,15 +873,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 const int nr = sh.n_rays;
                 const OverlayZeta oz{d.cand_flag, d.cand_z, d.zeta0};
                 for (int rr = wv; rr < nr; rr += kWaves) {
-                    const int r = v.rhit[rr];
+                    const int r = v.ray_at(rr);
                     const int s0 = v.ray_off[r];
                     const int npr = v.ray_off[r + 1] - s0;
+                    const double tsr = v.tS[r], sgr = v.sig[r], old_term = v.term[r];  // with the offsets
                     const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
                     if (lane == 0) {
                         v.cptS[r] = val;
-                        const double df = val - v.tS[r];
-                        const double sg = v.sig[r];
-                        v.cterm[r] = v.term[r];                      // kept to undo a rejection
+                        const double df = val - tsr;
+                        const double sg = sgr;
+                        v.cterm[r] = old_term;                       // kept to undo a rejection
                         v.term[r] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                         atomicAdd(&sh.ray_pts, npr);
                         if constexpr (!SMALL) atomicOr(&cmask[r >> 6], 1ull << (r & 63));  // an event of the walk
@@ -911,8 +1000,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // the hit tiles' maxima if the proposal is accepted (a tile = a DPP row)
                 const int nt = sh.n_tiles;
                 for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 256) {
-                    const int t = v.thit[i / kTilePts];
-                    const int sc = v.tstart[t];  // start << 5 | count
+                    const int sc = v.tile_rec(i / kTilePts).y;  // start << 5 | count
                     const int q = (sc >> 5) + (i % kTilePts);
                     unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
                     if (i % kTilePts < (sc & 31)) {
@@ -939,11 +1027,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     d.cand_flag[q] = 0;
                 }
                 if (fwd && action != tdchain::kChange) {
-                    for (int i = tid; i < nt; i += kChainThreads) v.tmaxd[v.thit[i]] = v.ctm[i];
+                    for (int i = tid; i < nt; i += kChainThreads) v.tmaxd[v.tile_rec(i).x] = v.ctm[i];
                     pend_sup = super_on;  // their super-tiles' maxima: at the top of the next iteration
                 }
                 for (int rr = tid; rr < nr; rr += kChainThreads) {
-                    const int r = v.rhit[rr];
+                    const int r = v.ray_at(rr);
                     v.ptS[r] = v.cptS[r];
                     v.rflag[r] = 0;
                 }
@@ -1001,7 +1089,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             } else {  // rejected: flags down, the changed rays get their old chi^2 terms back
                 for (int c = tid; c < nc; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
                 for (int rr = tid; rr < nr; rr += kChainThreads) {
-                    const int r = v.rhit[rr];
+                    const int r = v.ray_at(rr);
                     v.term[r] = v.cterm[r];
                     v.rflag[r] = 0;
                 }
@@ -1145,6 +1233,14 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
         e = hipGetLastError();
     }
     return e;
+}
+
+void chain_lds_sizes(const DevChain &d, int64_t out[4]) {
+    const LdsPlan a = lds_plan(d.ntiles, d.n, d.cap, true), b = lds_plan(d.ntiles, d.n, d.cap, false);
+    out[0] = (int64_t)a.total;      // LDS layout (tiles, rays, order mirrored)
+    out[1] = (int64_t)b.total;      // HBM layout
+    out[2] = b.super_lds ? 1 : 0;   // HBM layout with super-tiles in LDS
+    out[3] = (int64_t)(a.total <= kLdsBudget && d.lds_mode != 1);  // the layout a launch takes: 1 = LDS
 }
 
 hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s) {

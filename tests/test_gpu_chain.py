@@ -5,6 +5,8 @@ follow the HOST engine -- which evaluates every proposal with a full
 td_evaluate exactly as the reference does -- bit for bit: same accepted
 proposals, same phi after every run, same final model.  And the cached chain
 state must equal a from-scratch evaluate of its model at any time."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -192,6 +194,47 @@ def test_many_rays_chain_follows_host_engine(tt):
         assert dev.stats()["phi"] == host.stats()["phi"]
         assert dev.stats()["accepted"] == host.stats()["accepted"]
     assert same_models(dev.model(), host.model())
+    dev.close()
+    host.close()
+    ctx.close()
+
+
+def lds_plan(tt, ch):
+    out = (ctypes.c_int64 * 4)()
+    assert tt.lib().tdt_chain_lds(ch.h, out) == 0
+    return list(out)
+
+
+def test_bench_config_takes_lds_layout(tt, ds, ctx):
+    """bench.py's config 3 (381 rays, 5000 cells, max 10000) fits the LDS layout."""
+    prm = tt.define_TDstructrure().replace(max_cells=10000)
+    ch = make(tt, ctx, prm, tt.random_model(5000, 3), 3, tt.TD_ENGINE_DEVICE)
+    small, big, sup, layout = lds_plan(tt, ch)
+    assert small <= 160 * 1024 and layout == 1, (small, big)
+    ch.close()
+
+
+def test_stress_geometry_chain_follows_host_engine(tt):
+    """10k synthetic rays (the stress geometry): the HBM layout with super-tiles
+    in LDS and the chi^2 event walk, bit for bit the host engine over a few
+    hundred proposals (accepted ones commit the walk's segments and re-mark)."""
+    ds = tt.synthetic_rays(10000, seed=5)
+    ctx = tt.TdContext.from_datastruct(ds)
+    prm = tt.define_TDstructrure().replace(max_cells=3000)
+    model = tt.random_model(2000, 51)
+    dev = make(tt, ctx, prm, model, 51, tt.TD_ENGINE_DEVICE)
+    small, big, sup, layout = lds_plan(tt, dev)
+    assert layout == 0 and sup == 1, (small, big, sup)
+    host = make(tt, ctx, prm, model, 51, tt.TD_ENGINE_HOST)
+    for _ in range(4):
+        dev.run(75)
+        host.run(75)
+        assert dev.stats()["phi"] == host.stats()["phi"]
+        assert dev.stats()["accepted"] == host.stats()["accepted"]
+    assert same_models(dev.model(), host.model())
+    m = dev.model()
+    ptS, phi, _, _ = ctx.evaluate(m.cells())
+    assert phi == m.phi and np.array_equal(ptS, m.ptS)
     dev.close()
     host.close()
     ctx.close()
