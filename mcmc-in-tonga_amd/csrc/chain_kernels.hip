@@ -47,6 +47,10 @@ constexpr int kWaves = kChainThreads / 64;
 static_assert(kTilePts == 16, "a tile is one 16-lane DPP row (row_max_u64)");
 constexpr int kOrphanLds = 256; // orphan records kept in LDS (more: read back from HBM)
 constexpr int kListLds = 1024;  // rays in HBM: hit tiles / changed rays / hit super-tiles kept in LDS
+// The LDS layout could sum chi^2 with the event walk too; its tails are ~60 terms and the
+// one-wave binade scan with the early-rejection bound is faster there (measured: the walk
+// costs ~1.2k more cycles per proposal at 381 rays x 5000 cells)
+constexpr bool kSmallWalk = false;
 
 // A point whose nearest cell is removed or moved: re-searched in phase D.
 struct OrphanRec {
@@ -172,6 +176,10 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
     size_t o = align16(sizeof(Shared));
     L.scratch = o; o += align16(sizeof(double) * kWaves * 96);
     L.draws = o; o += align16(sizeof(tdchain::Draws) * 64);                     // 64 iterations ahead
+    if (!small || kSmallWalk) {  // the chi^2 walk's event words (exact_sum.h): static ones, kept; changed rays
+        L.smask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
+        L.cmask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
+    }
     if (small) {
         L.tlo = o; o += align16(sizeof(float) * 3 * ntiles);
         L.thi = o; o += align16(sizeof(float) * 3 * ntiles);
@@ -192,9 +200,7 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
         L.rflag = o; o += align16(sizeof(int) * n);
         L.rhit = o; o += align16(sizeof(int) * n);
         L.ord = o; o += align16(sizeof(int) * cap);
-    } else {  // the chi^2 walk's event words (exact_sum.h): static ones, kept; changed rays
-        L.smask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
-        L.cmask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
+    } else {
         // the first hit tiles as {tile, start << 5 | count, ray} records, the first changed rays
         size_t q = o;
         L.hrec = q; q += align16(sizeof(int4) * kListLds);
@@ -499,6 +505,7 @@ __device__ __forceinline__ float f32_up(double x) {
 
 template <bool SMALL>
 __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters) {
+    constexpr bool WALK = !SMALL || kSmallWalk;  // chi^2 by the event walk
     const DevChain &d = dptr[blockIdx.x];  // fields read from memory as needed, not pinned in registers
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Shared &sh = *reinterpret_cast<Shared *>(lds);
@@ -600,9 +607,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     float *smax = reinterpret_cast<float *>(lds + L.smax);  // >= the max of its tiles' maxima
     int *shit = reinterpret_cast<int *>(lds + L.shit);
     const bool super_on = !SMALL && L.super_lds;
-    if constexpr (!SMALL) {  // rays in HBM: the chi^2 walk's static event words of the current state
+    if constexpr (WALK) {  // the chi^2 walk's static event words of the current state
+        if constexpr (SMALL) __syncthreads();  // the terms above
         delta_marks(v.term, v.prefix, nullptr, n, smask, wv, delta_words(n), kWaves, lane);
         for (int w = tid; w < delta_words(n); w += kChainThreads) cmask[w] = 0ull;
+    }
+    if constexpr (!SMALL) {
         if (super_on) {  // super-tile boxes, and maxima = the max of their tiles' maxima
             for (int i = tid; i < 3 * NS; i += kChainThreads) {
                 slo[i] = d.super_lo[i];
@@ -645,11 +655,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     bool pend_sup = false;  // rays in HBM: its super-tiles' maxima not yet refreshed
     for (long long it = 0; it < iters; ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
-        if constexpr (!SMALL) {
+        if constexpr (WALK) {
             // the previous accepted proposal's partial sums (read again only in phase F,
             // after at least one barrier): off its critical path, before this one's tiles
-            if (pend_r) delta_commit<16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
+            if (pend_r) delta_commit<SMALL ? 1 : 16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
             pend_r = false;
+        }
+        if constexpr (!SMALL) {
             if (pend_sup) {  // its hit super-tiles: max of their tiles' new maxima (a tile row each)
                 const int par = (int)((it - 1) & 1), nsh = sh.n_super[par];
                 const bool all = nsh > kListLds;  // the list overflowed: every super-tile
@@ -885,7 +897,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         v.cterm[r] = old_term;                       // kept to undo a rejection
                         v.term[r] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                         atomicAdd(&sh.ray_pts, npr);
-                        if constexpr (!SMALL) atomicOr(&cmask[r >> 6], 1ull << (r & 63));  // an event of the walk
+                        if constexpr (WALK) atomicOr(&cmask[r >> 6], 1ull << (r & 63));  // an event of the walk
                     }
                 }
                 __syncthreads();
@@ -907,8 +919,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     double C = k0 > 0 ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
                     if (k0 < n) {
                         bool stopped = false;
-                        long long *rc = prof_on && SMALL ? &sh.prof[65] : nullptr;
-                        if constexpr (SMALL)
+                        long long *rc = prof_on && !WALK ? &sh.prof[65] : nullptr;
+                        if constexpr (!WALK)
                             C = wave_seq_sum(v.term + k0, n - k0, C, v.cprefix + k0, lane, &sh.early_reject, &stopped,
                                              rc);
                         else  // O(events), not O(tail): exact_sum.h delta_walk
@@ -983,7 +995,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // non-negative terms is within n ulps of any other association; above
                 // the rejection bound by a wide margin, the proposal is rejected
                 const int k0 = sh.k0;
-                if (SMALL && fwd && k0 < n) {
+                if (!WALK && fwd && k0 < n) {
                     double part = 0.0;
                     for (int k = k0 + lane; k < n; k += 64) part = part + v.term[k];
                     const double S = wave_sum_f64(part);
@@ -1035,7 +1047,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     v.ptS[r] = v.cptS[r];
                     v.rflag[r] = 0;
                 }
-                if constexpr (SMALL) {
+                if constexpr (!WALK) {
                     for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
                 } else if (fwd && k0 < n) {
                     pend_r = true;  // written at the top of the next iteration
@@ -1140,8 +1152,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         STAMP(6);
     }
 
-    if constexpr (!SMALL)
-        if (pend_r) delta_commit<16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
+    if constexpr (WALK) {
+        if (pend_r) delta_commit<SMALL ? 1 : 16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
+        if constexpr (SMALL) __syncthreads();  // the LDS sums are written back below
+    }
     // ---- leave the LDS copies behind (flags and grid are already clean) ----
     if constexpr (SMALL) {
         for (int i = tid; i < NT; i += kChainThreads) d.tile_maxd[i] = v.tmaxd[i];

@@ -1,0 +1,53 @@
+"""Diagnostic: phase cycles of the device chain when C chains share one GPU
+(td_chain_run_batch, one workgroup each), averaged over the chains, beside
+the single-chain numbers of profiles/chain_phases.py.  usage: batch_phases.py C iters"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import tonga  # noqa: E402
+
+PHASES = ["top", "B", "C", "D", "E", "F", "G"]
+
+
+def main():
+    C = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+    tt = tonga.load()
+    ds = tt.load_data_Tonga()
+    ctx = tt.TdContext.from_datastruct(ds)
+    prm = tt.define_TDstructrure().replace(max_cells=10000)
+    model = tt.random_model(5000, 3)
+    chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=50000 + j, chain=10000 + j), model) for j in range(C)]
+    tt.run_batch(chains, iters)
+    L = tt.lib()
+    outs0 = []
+    for c in chains:
+        o = (ctypes.c_int64 * 80)()
+        L.tdt_chain_profile(c.h, 1, o)
+        outs0.append(np.array(o[:], dtype=np.float64))
+    t0 = time.perf_counter()
+    tt.run_batch(chains, iters)
+    el = time.perf_counter() - t0
+    tot = np.zeros(80)
+    for c, o0 in zip(chains, outs0):
+        o = (ctypes.c_int64 * 80)()
+        L.tdt_chain_profile(c.h, 0, o)
+        tot += np.array(o[:], dtype=np.float64) - o0
+    cyc = tot[:7].copy()
+    cyc[6] += tot[12] + tot[13]
+    n = C * iters
+    print(json.dumps({"chains": C, "iters": iters, "us_per_iter_wall": el / iters * 1e6,
+                      "proposals_per_s": n / el,
+                      "cycles_per_iter_per_chain": {p: round(c / n, 1) for p, c in zip(PHASES, cyc)},
+                      "total": round(cyc.sum() / n, 1),
+                      "F per wave": [round(tot[56 + w] / n, 1) for w in range(8)]}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
