@@ -22,9 +22,10 @@ Also reported:
   full_evaluate -- the drop-in td_evaluate path (brute-force P x N nearest
                    search, MCsub.jl:123-185) on the same model: latency and
                    the FP64-VALU roofline of its dominant kernel nn_partial.
-  cpu_baseline  -- the CPU oracle (scalar C restatement of evaluate, 1 core)
-                   timed for ~--cpu-seconds: the reference's structure does
-                   one full evaluate per proposal.
+  cpu_baseline  -- the CPU oracle (scalar C restatement of evaluate), one
+                   chain per host core of the job's share (and on 1 core),
+                   ~--cpu-seconds in all: the reference's structure does one
+                   full evaluate per proposal.
 """
 import argparse
 import json
@@ -316,23 +317,53 @@ def stress(tt, chain_iters=2000):
     return res
 
 
+def host_cores():
+    """The host cores this job may use: the box exports its CPU share in
+    OMP_NUM_THREADS (16); os.cpu_count() reports the whole machine."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(n if n > 0 else 16, os.cpu_count() or 1))
+
+
 def cpu_baseline(ds, model, seconds):
+    """The reference's structure on the host: one full evaluate per proposal
+    (oracle/tstar_oracle.c, the scalar restatement of MCsub.jl:123-185), one
+    chain per core as main_inversion.jl:15's pmap runs them.  Threads call the
+    C oracle through ctypes, which releases the GIL, so they run in parallel.
+    Timed on 1 core, then on every core of the job's share."""
+    import threading
+
     import oracle  # CPU baseline leg only
 
-    o = oracle.lib()
+    oracle.lib()
     cells = model.cells()
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        oracle.evaluate(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig, cells)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    del o
-    return {"value": round(n / el, 3), "unit": "proposals/s", "cores": 1, "kind": "port",
-            "sample": "%d full evaluates (oracle/tstar_oracle.c, scalar FP64, -O2) of the same 381-ray x %d-cell "
-                      "model in %.1f s; the reference evaluates every proposal in full" % (n, len(cells[0]), el)}
+
+    def leg(threads, secs):
+        counts = [0] * threads
+        t0 = time.perf_counter()
+
+        def work(k):
+            while time.perf_counter() - t0 < secs:
+                oracle.evaluate(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig, cells)
+                counts[k] += 1
+
+        ts = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return sum(counts), time.perf_counter() - t0
+
+    n1, el1 = leg(1, seconds * 0.5)
+    cores = host_cores()
+    nc, elc = leg(cores, seconds * 0.5)
+    return {"value": round(nc / elc, 3), "unit": "proposals/s", "cores": cores, "kind": "port",
+            "single_core_value": round(n1 / el1, 3),
+            "sample": "full evaluates (oracle/tstar_oracle.c, scalar FP64, -O2) of the same 381-ray x %d-cell "
+                      "model, one chain per core: %d in %.1f s on %d cores, %d in %.1f s on 1 core; the reference "
+                      "evaluates every proposal in full" % (len(cells[0]), nc, elc, cores, n1, el1)}
 
 
 if __name__ == "__main__":

@@ -336,8 +336,11 @@ int device_setup(td_chain *ch) {
     d.seed = ch->prm.seed;
     d.chain = (uint32_t)ch->prm.chain;
 
-    e = hipHostMalloc(&ch->st_host, sizeof(ChainScalars), hipHostMallocDefault);
+    // pinned, mapped and coherent: k_chain_run writes its scalars here at the end of a launch
+    e = hipHostMalloc(&ch->st_host, sizeof(ChainScalars), hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) return hip_err(c, e, "hipHostMalloc(chain scalars)");
+    e = hipHostGetDevicePointer(reinterpret_cast<void **>(&d.st_host), ch->st_host, 0);
+    if (e != hipSuccess) return hip_err(c, e, "hipHostGetDevicePointer(chain scalars)");
     // ---- uploads ----
     const int N = (int)ch->x.size();
     std::vector<int> ident((size_t)cap), rank0((size_t)cap, -1);  // slots >= N are free
@@ -386,11 +389,9 @@ int device_setup(td_chain *ch) {
     return TD_OK;
 }
 
-int device_pull_scalars(td_chain *ch) {
-    td_ctx *c = ch->ctx;
-    hipError_t e = hipMemcpyAsync(ch->st_host, ch->st_dev, sizeof(ChainScalars), hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) return hip_err(c, e, "chain scalars");
+// the chain's scalars from its pinned mirror (written by k_chain_run at the end
+// of every launch, or copied by device_pull_scalars)
+void adopt_scalars(td_chain *ch) {
     const ChainScalars &s = *ch->st_host;
     ch->iter = s.iter;
     ch->phi = s.phi;
@@ -402,6 +403,14 @@ int device_pull_scalars(td_chain *ch) {
     ch->stats.ncells = s.ncells;
     ch->stats.phi = s.phi;
     ch->stats.bytes = s.bytes;
+}
+
+int device_pull_scalars(td_chain *ch) {
+    td_ctx *c = ch->ctx;
+    hipError_t e = hipMemcpyAsync(ch->st_host, ch->st_dev, sizeof(ChainScalars), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "chain scalars");
+    adopt_scalars(ch);
     return TD_OK;
 }
 
@@ -500,10 +509,11 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
     e = chain_run(&ch->dev, ch->dev_ptr, 1, iterations, ch->ctx->stream);
     if (tm) tm->end("chain_run", t0, ch->ctx->stream);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "k_chain_run launch");
-    const int64_t before = ch->stats.iterations;
-    int rc = device_pull_scalars(ch);
-    ch->stats.iterations = before + iterations;
-    return rc;
+    e = hipStreamSynchronize(ch->ctx->stream);  // the kernel wrote the scalars to st_host
+    if (e != hipSuccess) return hip_err(ch->ctx, e, "k_chain_run");
+    adopt_scalars(ch);
+    ch->stats.iterations += iterations;
+    return TD_OK;
 }
 
 int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterations) {
@@ -547,11 +557,10 @@ int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterati
     hipError_t e = chain_run(hd, static_cast<const DevChain *>(c->chain_desc), (int)nchains, iterations, c->stream);
     if (tm) tm->end("chain_run", t0, c->stream);
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (batch)");
+    TD_HIP(c, hipStreamSynchronize(c->stream));  // every chain wrote its scalars to its st_host
     for (int64_t b = 0; b < nchains; ++b) {
-        const int64_t before = chains[b]->stats.iterations;
-        int rc = device_pull_scalars(chains[b]);
-        chains[b]->stats.iterations = before + iterations;
-        if (rc) return rc;
+        adopt_scalars(chains[b]);
+        chains[b]->stats.iterations += iterations;
     }
     return TD_OK;
 }

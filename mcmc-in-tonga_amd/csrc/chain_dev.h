@@ -82,6 +82,7 @@ struct DevChain {
     int *rays_hit;
     int *ray_flag;
     ChainScalars *st;
+    ChainScalars *st_host;  // pinned host mirror (device address), written at the end of a launch
     tdchain::Params params;
     uint64_t seed;
     uint32_t chain;

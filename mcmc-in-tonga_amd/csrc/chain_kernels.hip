@@ -1180,6 +1180,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         s.nfree = sh.nfree;
         for (int k = 0; k < kProfSlots; ++k) s.prof[k] += sh.prof[k];
         s.prof[15] += sh.grid_fallbacks32;  // diagnostic: unproven grid searches
+        if (d.st_host) *d.st_host = s;  // the host's pinned mirror: no copy back per chain
     }
 }
 
