@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--batch-chains", type=int, default=256,
                     help="size of the extra many-chains-per-GPU measurement on rank 0 (0 = skip)")
     ap.add_argument("--batch-iters", type=int, default=1000)
+    ap.add_argument("--no-config4", dest="config4", action="store_false",
+                    help="skip the config-4 block (8 tempered replicas x 2000 cells, swap every 10, one GPU)")
     ap.add_argument("--no-stress", action="store_true",
                     help="skip the config-5 stress block (10k synthetic rays x 20k cells)")
     return ap.parse_args()
@@ -213,6 +215,8 @@ def main():
         out["full_evaluate"] = full_evaluate(tt, ctx, model, N)
     if rank == 0 and not a.no_stress:
         out["stress"] = stress(tt)
+    if rank == 0 and a.config4:
+        out["config4_tempering"] = tempering_config4(tt, ctx, ds)
     if rank == 0 and a.batch_chains > 0:
         out["many_chains"] = many_chains(tt, ctx, ds, prm, model, a.batch_chains, a.batch_iters)
     if rank == 0 and not a.no_cpu_baseline:
@@ -225,6 +229,36 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def tempering_config4(tt, ctx, ds, nrep=8, ncells=2000, swap_every=10, rounds=300):
+    """BASELINE config 4's ladder on ONE GPU: 8 tempered replicas x 2000 cells
+    (seeds 100 + replica), geometric T in [1, 8], a swap round every 10
+    proposals; the replicas run in one td_chain_run_batch launch per round, the
+    allgather is the identity in one process (the N-GPU runs put one rank per
+    GPU and gather over RCCL: tests/test_gpu_config4.py checks the two agree)."""
+    prm = tt.define_TDstructrure().replace(max_cells=2 * ncells)
+    chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=100 + g, chain=1 + g), tt.random_model(ncells, 100 + g))
+              for g in range(nrep)]
+    lad = tt.TemperingLadder(chains, tmax=8.0, seed=4242)
+    for _ in range(20):
+        lad.step(swap_every)
+    ctx.timing(enable=True, reset=True)
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        lad.step(swap_every)
+    el = time.perf_counter() - t0
+    launches, kms = ctx.timing(kernel="chain_run")
+    ctx.timing(enable=False)
+    res = {"replicas": nrep, "cells": ncells, "swap_every": swap_every, "rounds": rounds,
+           "proposals_per_s": round(nrep * swap_every * rounds / el, 1),
+           "ms_per_round": round(el / rounds * 1e3, 4),
+           "kernel_ms_per_round": round(kms / max(launches, 1), 4),
+           "temps": [round(t, 4) for t in lad.temps], "swap_rates": [round(r, 3) for r in lad.swap_rates()],
+           "cold_phi": chains[lad.cold_local()].stats()["phi"]}
+    for c in chains:
+        c.close()
+    return res
 
 
 def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3):

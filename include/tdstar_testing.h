@@ -78,6 +78,16 @@ int tdt_block_delta_sum(int device, const double *term, const double *term_old, 
 int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, double *prefix, double *C_end,
                      int *fallbacks);
 
+/* chi^2 (MCsub.jl:169-172) of a caller-given ptS[n] against the context's tS
+ * and allSig, through the device code that computes it in the product:
+ * path 0 the fused tail of td_evaluate's ray-sum kernel (n <= 2048), 1 the
+ * block-wide exact scan td_evaluate uses for long ray lists, 2 the device
+ * chain's starting-state prefix sums (k_chi2_prefix), 3 the chain's
+ * proposal-time one-wave scan (from k0 = 0 -> out[0], and restarted at
+ * k0 = n/2 on path 2's prefix -> out[1]).  Lets the tests pin the HIP code to
+ * the reference's own model.jld phi values.  1 <= n <= 4096.  Needs a GPU. */
+int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]);
+
 /* Nearest-cell method of td_evaluate / td_interpolate: 0 auto (bucket grid
  * from 256 cells on), 1 brute force (every point x every cell), 2 bucket grid.
  * All give the same answer (the lexicographic (distance, index) minimum). */

@@ -86,6 +86,7 @@ SIGNATURES = {
     "tdt_block_delta_sum": (ctypes.c_int, [ctypes.c_int, _pd, _pd, _pd, _pi32, _i64, _i64, _pd, _pd,
                                             ctypes.POINTER(ctypes.c_int64), _pi32]),
     "tdt_wave_seq_sum": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _d, _pd, _pd, _pi32]),
+    "tdt_chi2": (ctypes.c_int, [_vp, _pd, ctypes.c_int, _pd]),
     "tdt_accept": (ctypes.c_int, [ctypes.POINTER(TdChainParams), ctypes.c_int, _d, _d, _i64, _d, _d, _d, _d, _d]),
 }
 

@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "chain_dev.h"
 #include "ctx.h"
 
 namespace {
@@ -562,6 +563,33 @@ int tdt_block_delta_sum(int device, const double *term, const double *term_old, 
     *events = ev;
     (void)hipFree(buf);
     return e == hipSuccess ? TD_OK : TD_ERR_HIP;
+}
+
+int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]) {
+    if (!ctx || !out || (!ptS && ctx->g.n > 0) || path < 0 || path > 3) return set_err(ctx, TD_ERR_ARG, "tdt_chi2");
+    const int64_t n = ctx->g.n;
+    if (n < 1 || n > 4096 || (path == 0 && n > 2048)) return set_err(ctx, TD_ERR_ARG, "tdt_chi2: n out of range");
+    TD_HIP(ctx, hipSetDevice(ctx->device));
+    double *dp = nullptr, *scratch = nullptr, *dout = nullptr;
+    const size_t sn = 3 * (size_t)n + 8 + 1024 / sizeof(double);
+    hipError_t e = hipMalloc(&dp, sizeof(double) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&scratch, sizeof(double) * sn);
+    if (e == hipSuccess) e = hipMalloc(&dout, sizeof(double) * 2);
+    if (e == hipSuccess) e = hipMemsetAsync(dout, 0, sizeof(double) * 2, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dp, ptS, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) {
+        if (path <= 1)
+            e = test_chi2(dp, ctx->g.tS, ctx->g.sig, (int)n, path, scratch, dout, ctx->stream);
+        else
+            e = test_chain_chi2(dp, ctx->g.tS, ctx->g.sig, (int)n, path, scratch, dout, ctx->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (dp) (void)hipFree(dp);
+    if (scratch) (void)hipFree(scratch);
+    if (dout) (void)hipFree(dout);
+    if (e != hipSuccess) return hip_err(ctx, e, "tdt_chi2");
+    return TD_OK;
 }
 
 int tdt_set_nn_method(td_ctx *ctx, int method) {

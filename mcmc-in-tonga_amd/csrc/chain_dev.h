@@ -102,6 +102,14 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
 // (workgroup b runs chain b).  `host` = the descriptors, `dev` = their device
 // copy, contiguous (the kernel reads its fields from global memory).
 hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s);
+// Testing: the chain's chi^2 code on a caller-given ptS (n <= 4096) --
+// path 2: k_chi2_prefix (the starting state's sequential prefix sums, what
+// chain_full_state runs), 3: the proposal-time sum (the terms of MCsub.jl:171,
+// then the one-wave exact scan of phase F from k0 = 0, and again from
+// k0 = n/2 on top of path 2's prefix[k0-1]).  out[0] = phi, out[1] = phi of
+// the restart from n/2 (path 3 only).  scratch: 3n + 16 doubles.
+hipError_t test_chain_chi2(const double *ptS, const double *tS, const double *sig, int n, int path, double *scratch,
+                           double *out, hipStream_t s);
 // LDS bytes of the two layouts, whether super-tiles fit, and the layout chain_run takes.
 void chain_lds_sizes(const DevChain &d, int64_t out[4]);
 

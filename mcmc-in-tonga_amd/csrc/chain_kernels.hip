@@ -1219,7 +1219,51 @@ __global__ void k_tile_max(const int *__restrict__ tile_start, int ntiles, const
     tile_maxd[t] = mx;
 }
 
+// The proposal-time chi^2 of phase F on a caller-given ptS (testing): terms as
+// phase E writes them, the one-wave exact scan from k0 = 0 and from k0 = n/2
+// (C0 = the sequential prefix[k0 - 1] of k_chi2_prefix).
+__global__ __launch_bounds__(64) void k_test_chain_chi2(const double *__restrict__ ptS, const double *__restrict__ tS,
+                                                        const double *__restrict__ sig, int n,
+                                                        const double *__restrict__ prefix, double *term,
+                                                        double *cprefix, double *out) {
+    const int lane = threadIdx.x;
+    for (int r = lane; r < n; r += 64) {
+        const double df = ptS[r] - tS[r];
+        const double sg = sig[r];
+        term[r] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
+    }
+    __syncthreads();
+    bool stopped = false;
+    const double a = wave_seq_sum(term, n, 0.0, cprefix, lane, nullptr, &stopped);
+    const int k0 = n / 2;
+    stopped = false;
+    const double b = k0 < n ? wave_seq_sum(term + k0, n - k0, k0 > 0 ? prefix[k0 - 1] : 0.0, cprefix + k0, lane, nullptr,
+                                           &stopped)
+                            : a;
+    if (lane == 0) {
+        out[0] = a;
+        out[1] = b;
+    }
+}
+
 }  // namespace
+
+hipError_t test_chain_chi2(const double *ptS, const double *tS, const double *sig, int n, int path, double *scratch,
+                           double *out, hipStream_t s) {
+    if (n < 1 || n > 4096) return hipErrorInvalidValue;
+    double *prefix = scratch, *term = scratch + n, *cpre = scratch + 2 * n;
+    ChainScalars *st = reinterpret_cast<ChainScalars *>(scratch + 3 * n + 8);  // 16-byte aligned slot
+    static_assert(sizeof(ChainScalars) <= 1024, "scratch slot");
+    if (path == 2) {
+        hipLaunchKernelGGL(k_chi2_prefix, dim3(1), dim3(256), 0, s, ptS, tS, sig, n, prefix, st);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return hipMemcpyAsync(out, &st->phi, sizeof(double), hipMemcpyDeviceToDevice, s);
+    }
+    hipLaunchKernelGGL(k_chi2_prefix, dim3(1), dim3(256), 0, s, ptS, tS, sig, n, prefix, st);
+    hipLaunchKernelGGL(k_test_chain_chi2, dim3(1), dim3(64), 0, s, ptS, tS, sig, n, prefix, term, cpre, out);
+    return hipGetLastError();
+}
 
 hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, hipStream_t s) {
     Geometry g;

@@ -153,6 +153,11 @@ hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *pre
 hipError_t test_wave_delta_sum(const double *term, const double *old, const int *chg, int cnt, double C0,
                                double *prefix, double *C_end);
 hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast);
+// Testing: phi of a caller-given ptS through the evaluate path's chi^2 code --
+// path 0: the fused last-workgroup tail (n <= 2048), 1: k_chi2 (block-wide
+// exact scan, long ray lists).  terms: n doubles of scratch.
+hipError_t test_chi2(const double *ptS, const double *tS, const double *sig, int n, int path, double *terms,
+                     double *phi, hipStream_t s);
 hipError_t test_block_delta(const double *term, const double *term_old, double *old, const int *chg, int k0, int n,
                             double *cprefix, double *C_end, long long *events, int *mask_ok);
 

@@ -173,6 +173,25 @@ __global__ __launch_bounds__(256) void k_ray_sums(const int *__restrict__ ray_of
 constexpr int kChi2Threads = 1024;
 constexpr int kChi2Lds = 2048;  // fused up to this many rays
 
+// The last workgroup's chi^2 (n <= kChi2Lds): the terms of MCsub.jl:171 in
+// LDS, then one wave adds them in k order (exact_sum.h wave_seq_sum).  Every
+// thread of the block calls it; thread 0's return value is phi.
+__device__ __forceinline__ double chi2_fused_tail(const double *ptS, const double *__restrict__ tS,
+                                                  const double *__restrict__ sig, int n, double *lterm) {
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const double d = ptS[k] - tS[k];
+        const double sg = sig[k];
+        lterm[k] = ((d * d) * 1.0) / (sg * sg);  // MCsub.jl:171
+    }
+    __syncthreads();
+    double C = 0.0;
+    if ((threadIdx.x >> 6) == 0) {
+        bool stopped = false;
+        C = wave_seq_sum(lterm, n, 0.0, nullptr, (int)(threadIdx.x & 63), nullptr, &stopped);
+    }
+    return C;
+}
+
 __global__ __launch_bounds__(256) void k_ray_sums_chi2(const int *__restrict__ ray_off, int n,
                                                        const double *__restrict__ w,
                                                        const double *__restrict__ z0, double *ptS,
@@ -201,23 +220,22 @@ __global__ __launch_bounds__(256) void k_ray_sums_chi2(const int *__restrict__ r
     __syncthreads();
     if (!last) return;
     __threadfence();  // every other workgroup's ptS
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const double d = ptS[k] - tS[k];
-        const double sg = sig[k];
-        lterm[k] = ((d * d) * 1.0) / (sg * sg);  // MCsub.jl:171
-    }
-    __syncthreads();
-    double C = 0.0;
-    if (wv == 0) {
-        bool stopped = false;
-        C = wave_seq_sum(lterm, n, 0.0, nullptr, lane, nullptr, &stopped);
-    }
+    const double C = chi2_fused_tail(ptS, tS, sig, n, lterm);
     if (threadIdx.x == 0) {
         *phi = C;
         if (host_out) host_out[0] = C;
         *done = 0u;  // ready for the next evaluation
         __threadfence_system();
     }
+}
+
+// The chi^2 of the fused evaluate on a caller-given ptS (testing: pins this
+// exact code to model.jld's phi values, tdt_chi2).
+__global__ __launch_bounds__(256) void k_test_chi2_fused(const double *ptS, const double *__restrict__ tS,
+                                                         const double *__restrict__ sig, int n, double *phi) {
+    __shared__ double lterm[kChi2Lds];
+    const double C = chi2_fused_tail(ptS, tS, sig, n, lterm);
+    if (threadIdx.x == 0) *phi = C;
 }
 
 __global__ __launch_bounds__(kChi2Threads) void k_chi2(const double *__restrict__ ptS,
@@ -339,6 +357,17 @@ hipError_t test_wave_delta_sum(const double *term, const double *old, const int 
 
 hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fallbacks) {
     hipLaunchKernelGGL(k_test_wave_seq_sum, dim3(1), dim3(64), 0, nullptr, term, cnt, C0, prefix, C_end, fallbacks);
+    return hipGetLastError();
+}
+
+hipError_t test_chi2(const double *ptS, const double *tS, const double *sig, int n, int path, double *terms,
+                     double *phi, hipStream_t s) {
+    if (path == 0) {
+        if (n > kChi2Lds) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_test_chi2_fused, dim3(1), dim3(256), 0, s, ptS, tS, sig, n, phi);
+    } else {
+        hipLaunchKernelGGL(k_chi2, dim3(1), dim3(kChi2Threads), 0, s, ptS, tS, sig, n, terms, phi, nullptr);
+    }
     return hipGetLastError();
 }
 

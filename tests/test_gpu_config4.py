@@ -1,0 +1,110 @@
+"""BASELINE config 4 on the GPU: 8 tempered replicas x 2000 cells, geometric
+T in [1, 8], a temperature swap every 10 proposals.
+
+* one process: the 8 DEVICE replicas (one td_chain_run_batch launch per
+  round) make exactly the moves and swaps of 8 HOST replicas, which evaluate
+  every proposal in full as the reference does (TD_inversion_function.jl:93,
+  141,191,238);
+* two fresh child processes (subprocess, gloo, both on device 0, 4 replicas
+  each) exchanging phi through torch.distributed: every rank sees the same
+  gathered vector and the ladder's trace equals the one-process ladder.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from tempering_worker import ladder_chains  # noqa: E402
+
+NREP, NCELLS, SWAP_EVERY, ROUNDS = 8, 2000, 10, 40
+
+
+def trace_of(tt, chains):
+    lad = tt.TemperingLadder(chains, tmax=8.0, seed=4242)
+    assert lad.batch or chains[0].params.engine == tt.TD_ENGINE_HOST
+    trace = []
+    for _ in range(ROUNDS):
+        phis = lad.step(SWAP_EVERY)
+        trace.append([[float(x) for x in phis], [int(x) for x in lad.levels]])
+    return trace, lad
+
+
+@pytest.fixture(scope="module")
+def ctx(tt, ds):
+    c = tt.TdContext.from_datastruct(ds)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def device_run(tt, ctx):
+    prm = tt.define_TDstructrure().replace(max_cells=2 * NCELLS)
+    chains = ladder_chains(tt, ctx, prm, 0, NREP, NCELLS, tt.TD_ENGINE_DEVICE)
+    trace, lad = trace_of(tt, chains)
+    models = [c.model() for c in chains]
+    out = dict(trace=trace, models=models, rates=lad.swap_rates(), stats=[c.stats() for c in chains])
+    for c in chains:
+        c.close()
+    return out
+
+
+def test_config4_ladder_device_matches_host(tt, ctx, device_run):
+    prm = tt.define_TDstructrure().replace(max_cells=2 * NCELLS)
+    chains = ladder_chains(tt, ctx, prm, 0, NREP, NCELLS, tt.TD_ENGINE_HOST)
+    trace, lad = trace_of(tt, chains)
+    assert trace == device_run["trace"]
+    for c, m, st in zip(chains, device_run["models"], device_run["stats"]):
+        h = c.model()
+        assert np.array_equal(h.xCell, m.xCell) and np.array_equal(h.zeta, m.zeta)
+        assert c.stats()["accepted"] == st["accepted"] and c.stats()["proposed"] == st["proposed"]
+        c.close()
+    assert lad.swap_rates() == device_run["rates"]
+    assert sum(sum(st["accepted"]) for st in device_run["stats"]) > 0
+    assert any(r > 0 for r in device_run["rates"])  # temperatures actually moved
+    assert sorted(device_run["trace"][-1][1]) == list(range(NREP))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(400)
+def test_config4_two_processes_gloo_match_one_process(tt, device_run, tmp_path):
+    import torch.distributed  # noqa: F401  (warm the import before two children load it at once)
+
+    world, local, port = 2, NREP // 2, _free_port()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "tempering_worker.py"), str(r), str(world),
+                               str(port), str(tmp_path / ("r%d.json" % r)), str(local), str(ROUNDS),
+                               str(SWAP_EVERY), str(NCELLS)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT)
+             for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(o.decode(errors="replace"))
+    assert all(p.returncode == 0 for p in procs), outs
+    r = [json.load(open(tmp_path / ("r%d.json" % k))) for k in range(world)]
+    assert r[0]["trace"] == r[1]["trace"]  # every rank gathered the same phis and made the same swaps
+    assert r[0]["trace"] == device_run["trace"]  # ... and they are the one-process ladder's
+    ms = device_run["models"]
+    assert r[0]["ncells"] + r[1]["ncells"] == [len(m.xCell) for m in ms]
+    assert r[0]["zeta_sum"] + r[1]["zeta_sum"] == [float(sum(m.zeta)) for m in ms]
