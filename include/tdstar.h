@@ -152,7 +152,9 @@ int td_rasterize(td_ctx *ctx, int64_t nmodels, const int64_t *cell_off, const do
 
 /* ------------------------------------------------------------------------
  * rj-MCMC chain -- replaces TD_inversion_function.jl:7-305 (one chain) for
- * prior == 1 (uniform), the default (define_TDstructure.jl:52).  The chain
+ * the three priors of define_TDstructure.jl:15 (1 uniform, the default; 2
+ * normal; 3 exponential: TD_inversion_function.jl:91-119, 150-172, 194-212,
+ * MCsub.jl:97-108).  The chain
  * state (cells, per-point nearest-cell cache, ptS, phi) lives in device
  * memory; proposals are evaluated incrementally (birth: one new cell vs the
  * cache; death/move: re-search only the points whose cell changed; change:
@@ -167,7 +169,7 @@ typedef struct td_chain_params {
     int32_t zeta_scale;    /* 50 */
     int32_t max_cells;     /* 100 */
     int32_t min_cells;     /* 5 */
-    int32_t prior;         /* only 1 (uniform) is supported: TD_ERR_ARG otherwise */
+    int32_t prior;         /* 1 uniform, 2 normal, 3 exponential (TD_ERR_ARG otherwise) */
     double n_iter, burn_in, keep_each;
     /* xVec/yVec/zVec extents (DataStruct.xVec etc., min(xVec...), max(xVec...)) */
     double xmin, xmax, ymin, ymax, zmin, zmax;
@@ -194,6 +196,8 @@ typedef struct td_chain_stats {
     double phi;                /* current model */
     int64_t ncells;
     int64_t bytes;             /* DEVICE engine: algorithmic global-memory bytes read by the proposals */
+    int32_t last_action;       /* Model.action of the last iteration: the drawn action 1..4 (:72-73), 0 before any */
+    int32_t last_accept;       /* Model.accept of the last iteration: 1 if its proposal was accepted (:74,123,...) */
 } td_chain_stats;
 
 /* Start a chain from the given model (cells may be NULL/0 to draw a starting

@@ -42,7 +42,7 @@ class TdChainParams(ctypes.Structure):
 
 class TdChainStats(ctypes.Structure):
     _fields_ = [("iterations", _i64), ("evaluations", _i64), ("accepted", _i64 * 5), ("proposed", _i64 * 5),
-                ("phi", _d), ("ncells", _i64), ("bytes", _i64)]
+                ("phi", _d), ("ncells", _i64), ("bytes", _i64), ("last_action", _i32), ("last_accept", _i32)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/*.h

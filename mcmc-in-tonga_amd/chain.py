@@ -6,7 +6,7 @@ the reference does).  ``TD_inversion_function(TD_parameters, dataStruct,
 chain)`` keeps the reference's signature and bookkeeping: burn-in, thinning
 into ``model_hist`` (copies, not the aliased references the reference
 pushes, TD_inversion_function.jl:280), progress lines every ``print_each``,
-and optional checkpoint/resume (npz, TD_inversion_function.jl:41-67,282-294).
+and optional JLD checkpoint/resume (TD_inversion_function.jl:41-67,282-294).
 """
 import ctypes
 import glob
@@ -81,7 +81,8 @@ class Chain:
         s = TdChainStats()
         check(lib().td_chain_stats_get(self.h, ctypes.byref(s)), self.ctx.h)
         return dict(iterations=s.iterations, evaluations=s.evaluations, accepted=list(s.accepted)[1:],
-                    proposed=list(s.proposed)[1:], phi=s.phi, ncells=s.ncells, bytes=s.bytes)
+                    proposed=list(s.proposed)[1:], phi=s.phi, ncells=s.ncells, bytes=s.bytes,
+                    last_action=s.last_action, last_accept=s.last_accept)
 
     def model(self):
         cap = max(int(self.params.max_cells), self.stats()["ncells"]) + 1
@@ -95,6 +96,9 @@ class Chain:
         m = Model(float(k), arrs[0][:k].copy(), arrs[1][:k].copy(), arrs[2][:k].copy(), arrs[3][:k].copy())
         m.phi = phi.value
         m.ptS = ptS[:self.ctx.n].copy()
+        st = self.stats()
+        if st["last_action"] > 0:  # model.action / model.accept of the last iteration (:73-74)
+            m.action, m.accept = st["last_action"], st["last_accept"]
         return m
 
     def set_temperature(self, T):
@@ -125,76 +129,108 @@ def build_starting(TD_parameters, dataStruct, seed=1, chain=1):
 
 
 def TD_inversion_function(TD_parameters, dataStruct, chain, seed=None, model=None, engine=_lib.TD_ENGINE_DEVICE,  # noqa: N802
-                          checkpoint_dir=None, verbose=False, temperature=1.0):
-    """TD_inversion_function.jl:7-305: one chain; returns model_hist (list of Model copies)."""
+                          checkpoint_dir=None, verbose=False, temperature=1.0, stop_after=None):
+    """TD_inversion_function.jl:7-305: one chain; returns model_hist (list of Model copies).
+
+    Bookkeeping as the reference's loop (:275-298): from iteration burn_in on,
+    model_num counts iterations and every keep_each-th model is saved into
+    model_hist; with ``checkpoint_dir`` a JLD checkpoint
+    ``chain<c>_iter<it>_<pct>%.jld`` is written at the 1st saved model and at
+    every 10 % of them (:282-287: model, dataStruct, iter, saved_#,
+    model_num, model_hist, burnin = true), and before burn-in every
+    print_each iterations (:289-294: model, dataStruct, iter, burnin =
+    false).  At the start the newest checkpoint of this chain is resumed
+    (:41-67); all but the newest two are deleted (:53-55).
+
+    Deliberate differences: the resumed loop starts at iter + 1 (the
+    reference re-runs the saved iteration, :59,70; with the counter-based RNG
+    starting after it continues the interrupted chain exactly); "newest" is the
+    highest iteration number, not the last name in lexicographic order (:51,
+    which ranks iter1000 before iter900), and only this chain's files match
+    (glob("chain1*") also matches chain10..., :41).  The geometry of the
+    checkpoint's dataStruct is the caller's (it never changes: action 5 is
+    unreachable, :72).  ``stop_after``: return after that iteration (testing a
+    crash and resume)."""
+    from . import jld
+
     ctx = context_for(dataStruct)
     seed = chain * 7919 + 1 if seed is None else seed
     prm = chain_params(TD_parameters, dataStruct, seed=seed, chain=chain, temperature=temperature, engine=engine)
-    n_iter, burn_in, keep = int(TD_parameters.n_iter), int(TD_parameters.burn_in), int(TD_parameters.keep_each)
+    n_iter, keep = int(TD_parameters.n_iter), int(TD_parameters.keep_each)
+    B = float(TD_parameters.burn_in)
     print_each = int(TD_parameters.print_each)
-    num_models = int((TD_parameters.n_iter - TD_parameters.burn_in) / TD_parameters.keep_each)
-    model_hist, it0 = [], 1
+    num_models = int((TD_parameters.n_iter - TD_parameters.burn_in) / TD_parameters.keep_each)  # :25
+    model_hist, it0, model_num, used_num = [], 1, 0, 0
     ckpt = _latest_checkpoint(checkpoint_dir, chain) if checkpoint_dir else None
     if ckpt is not None:  # :41-67 resume
-        z = np.load(ckpt, allow_pickle=False)
-        model = Model(float(len(z["xCell"])), z["xCell"], z["yCell"], z["zCell"], z["zeta"])
-        it0 = int(z["iter"]) + 1
-        prm.seed = int(z["seed"])
-        for k in range(int(z["n_hist"])):
-            o = z["hist_off"]
-            sl = slice(o[k], o[k + 1])
-            model_hist.append(Model(float(o[k + 1] - o[k]), z["hx"][sl], z["hy"][sl], z["hz"][sl], z["hzeta"][sl],
-                                    phi=float(z["hphi"][k])))
+        c = jld.load_checkpoint(ckpt)
+        model = c["model"]
+        it0 = int(c["iter"]) + 1
+        if c["burnin"]:
+            model_hist, used_num, model_num = list(c["model_hist"]), c["saved"], c["model_num"]
     prm.start_iter = it0  # the counter-based RNG continues exactly where the checkpoint stopped
     ch = Chain(ctx, prm, model)
-    model_num = 0
+
+    def current():
+        m = ch.model()
+        m.tS = dataStruct.tS
+        m.likelihood = ctx.likelihood_const if TD_parameters.debug_prior != 1 else 1.0
+        return m
+
+    last = n_iter if stop_after is None else min(n_iter, int(stop_after))
     it = it0
-    while it <= n_iter:
-        # run up to the next bookkeeping point in one device launch
-        nxt = n_iter
-        if it < burn_in:
-            nxt = min(nxt, burn_in)
-        else:
-            nxt = min(nxt, it + (keep - 1 - (it - burn_in) % keep) if keep > 0 else n_iter)
+    while it <= last:
+        # run up to the next iteration with bookkeeping, in one device launch
+        nxt = last
+        if it < B:  # pre-burn-in: checkpoints every print_each (:289)
+            nxt = min(nxt, int(np.ceil(B)) - 1)
+        elif keep > 0:  # the next saved model: model_num + (nxt - it + 1) = 0 mod keep
+            nxt = min(nxt, it + (keep - model_num % keep) - 1)
         if print_each > 0:
             nxt = min(nxt, ((it + print_each - 1) // print_each) * print_each)
         nxt = max(nxt, it)
         ch.run(nxt - it + 1)
-        it_done = nxt
-        if it_done >= burn_in:
-            model_num = it_done - burn_in + 1
+        if nxt >= B:  # :276-288
+            model_num += nxt - it + 1
             if keep > 0 and model_num % keep == 0:
-                m = ch.model()
-                m.tS = dataStruct.tS
-                m.likelihood = ctx.likelihood_const
+                used_num += 1
+                m = current()
                 model_hist.append(m)
-                if checkpoint_dir and (len(model_hist) == 1 or (100 * len(model_hist) / max(num_models, 1)) % 10 < 1e-9):
-                    _save_checkpoint(checkpoint_dir, chain, it_done, n_iter, m, model_hist, prm.seed)
-        if verbose and print_each > 0 and it_done % print_each == 0:
-            print("Chain #%d at %g%% with a phi of %r" % (chain, 100 * it_done / n_iter, ch.stats()["phi"]))
-        it = it_done + 1
+                if checkpoint_dir and ((100 * used_num / num_models) % 10 < 1e-9 or used_num == 1):
+                    os.makedirs(checkpoint_dir, exist_ok=True)
+                    name = "chain%d_iter%d_%r%%.jld" % (chain, nxt, 100 * float(nxt) / float(TD_parameters.n_iter))
+                    jld.save_checkpoint(os.path.join(checkpoint_dir, name), m, dataStruct, float(nxt), True,
+                                        model_hist, used_num, model_num)
+        elif checkpoint_dir and print_each > 0 and nxt % print_each == 0:  # :289-294
+            os.makedirs(checkpoint_dir, exist_ok=True)
+            name = "chain%d_iter%d_%d%%.jld" % (chain, nxt, int(100 * nxt / TD_parameters.n_iter))
+            jld.save_checkpoint(os.path.join(checkpoint_dir, name), current(), dataStruct, nxt, False)
+        if verbose and print_each > 0 and nxt % print_each == 0:  # :296-298
+            print("Chain #%d at %r%% with a phi of %r" % (chain, 100 * nxt / TD_parameters.n_iter, ch.stats()["phi"]))
+        it = nxt + 1
     ch.close()
     return model_hist
 
 
+def _ckpt_iter(f):
+    return int(os.path.basename(f).split("_iter")[1].split("_")[0])
+
+
 def _latest_checkpoint(d, chain):
-    # exact chain prefix (the reference's glob("chain1*") also matches chain10..., :41)
-    files = sorted(glob.glob(os.path.join(d, "chain%d_iter*.npz" % chain)),
-                   key=lambda f: int(os.path.basename(f).split("_iter")[1].split("_")[0]))
+    """The newest checkpoint of this chain (highest iteration); all but the
+    newest two are removed, as TD_inversion_function.jl:53-55 does."""
+    files = [f for f in glob.glob(os.path.join(d, "chain%d_iter*.jld" % chain))
+             if os.path.basename(f).startswith("chain%d_iter" % chain)]
+    files.sort(key=_ckpt_iter)
+    for f in files[:-2]:
+        os.remove(f)
     return files[-1] if files else None
 
 
-def _save_checkpoint(d, chain, it, n_iter, model, hist, seed):
-    os.makedirs(d, exist_ok=True)
-    off = np.concatenate([[0], np.cumsum([len(m.xCell) for m in hist])]).astype(np.int64)
-    path = os.path.join(d, "chain%d_iter%d_%g%%.npz" % (chain, it, 100 * it / n_iter))
-    np.savez(path, xCell=model.xCell, yCell=model.yCell, zCell=model.zCell, zeta=model.zeta, iter=it, seed=seed,
-             n_hist=len(hist), hist_off=off, hx=np.concatenate([m.xCell for m in hist]),
-             hy=np.concatenate([m.yCell for m in hist]), hz=np.concatenate([m.zCell for m in hist]),
-             hzeta=np.concatenate([m.zeta for m in hist]), hphi=np.array([m.phi for m in hist]))
-    for f in glob.glob(os.path.join(d, "chain%d_iter*.npz" % chain)):  # keep the newest only (:53-55)
-        if f != path:
-            os.remove(f)
+def delete_checkpoints(d):
+    """main_inversion.jl:21-22: remove every chain*jld checkpoint after the run."""
+    for f in glob.glob(os.path.join(d, "chain*.jld")):
+        os.remove(f)
 
 
 def main_inversion(TD_parameters=None, dataStruct=None, out="model.jld", checkpoint_dir=None,  # noqa: N803
@@ -214,4 +250,6 @@ def main_inversion(TD_parameters=None, dataStruct=None, out="model.jld", checkpo
     maps = plot_model_hist(models, dataStruct, TD_parameters, 20.0)
     if out:
         jld.save(out, models)
+    if checkpoint_dir:
+        delete_checkpoints(checkpoint_dir)
     return models, maps

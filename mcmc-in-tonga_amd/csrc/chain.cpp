@@ -52,6 +52,7 @@ tdchain::Params make_params(const td_chain_params &p) {
     P.debug_prior = p.debug_prior;
     P.max_cells = p.max_cells;
     P.min_cells = p.min_cells;
+    P.prior = p.prior;
     P.zeta_scale = (double)p.zeta_scale;
     // TD_inversion_function.jl:22: zeta_scale * sig / 100 (Int*Int, then /)
     P.sig_zeta = (double)(p.zeta_scale * p.sig) / 100.0;
@@ -64,8 +65,16 @@ tdchain::Params make_params(const td_chain_params &p) {
     P.zr = ((double)p.sig / 100.0) * (p.zmax - p.zmin);
     P.temperature = p.temperature > 0.0 ? p.temperature : 1.0;
     const double two_pi_sqrt = 2.5066282746310002;
-    P.log_prior_birth = std::log((P.sig_zeta * two_pi_sqrt) / P.zeta_scale);
-    P.log_prior_death = std::log(P.zeta_scale / (P.sig_zeta * two_pi_sqrt));
+    if (p.prior == tdchain::kNormal) {  // :107, :160
+        P.log_prior_birth = std::log(P.sig_zeta / P.zeta_scale);
+        P.log_prior_death = std::log(P.zeta_scale / P.sig_zeta);
+    } else if (p.prior == tdchain::kExponential) {  // :113, :166
+        P.log_prior_birth = std::log((two_pi_sqrt * P.sig_zeta) / P.zeta_scale);
+        P.log_prior_death = std::log(P.zeta_scale / (two_pi_sqrt * P.sig_zeta));
+    } else {  // uniform :96, :151
+        P.log_prior_birth = std::log((P.sig_zeta * two_pi_sqrt) / P.zeta_scale);
+        P.log_prior_death = std::log(P.zeta_scale / (P.sig_zeta * two_pi_sqrt));
+    }
     tdchain::params_derived(P);
     return P;
 }
@@ -89,7 +98,12 @@ void build_starting(td_chain *ch) {
         ch->x[(size_t)i] = P.xmin + (P.xmax - P.xmin) * d.u_a;  // :92-94
         ch->y[(size_t)i] = P.ymin + (P.ymax - P.ymin) * d.u_b;
         ch->z[(size_t)i] = P.zmin + (P.zmax - P.zmin) * d.u_c;
-        ch->zeta[(size_t)i] = d.u_zeta * P.zeta_scale;  // :100
+        if (P.prior == tdchain::kNormal)  // :104 rand(Normal(0, zeta_scale))
+            ch->zeta[(size_t)i] = 0.0 + P.zeta_scale * d.z_zeta;
+        else if (P.prior == tdchain::kExponential)  // :107 -log(rand) * zeta_scale
+            ch->zeta[(size_t)i] = -tdchain::det_log(d.u_zeta) * P.zeta_scale;
+        else  // :100 rand * zeta_scale
+            ch->zeta[(size_t)i] = d.u_zeta * P.zeta_scale;
     }
 }
 
@@ -115,6 +129,8 @@ int host_iteration(td_chain *ch) {
     tdchain::Proposal p = tdchain::propose(P, dr, N);
     ch->iter += 1;
     ch->stats.iterations += 1;
+    ch->stats.last_action = p.action;  // model.action = action; model.accept = 0 (:73-74)
+    ch->stats.last_accept = 0;
     if (!p.active) return TD_OK;
     ch->stats.proposed[p.action] += 1;
     double czeta = 0.0, zeta_killed = 0.0, zetanew = 0.0;
@@ -156,6 +172,7 @@ int host_iteration(td_chain *ch) {
         ch->phi = phi_n;
         ch->ptS.swap(ptS_n);
         ch->stats.accepted[p.action] += 1;
+        ch->stats.last_accept = 1;
     }
     return TD_OK;
 }
@@ -403,6 +420,8 @@ void adopt_scalars(td_chain *ch) {
     ch->stats.ncells = s.ncells;
     ch->stats.phi = s.phi;
     ch->stats.bytes = s.bytes;
+    ch->stats.last_action = s.last_action;
+    ch->stats.last_accept = s.last_accept;
 }
 
 int device_pull_scalars(td_chain *ch) {
@@ -433,7 +452,8 @@ int td_chain_create(td_chain **out, td_ctx *ctx, const td_chain_params *params, 
     if (!out || !ctx || !params) return set_err(ctx, TD_ERR_ARG, "td_chain_create: NULL argument");
     *out = nullptr;
     const td_chain_params &p = *params;
-    if (p.prior != 1) return set_err(ctx, TD_ERR_ARG, "td_chain_create: only prior == 1 (uniform) is supported");
+    if (p.prior < 1 || p.prior > 3)
+        return set_err(ctx, TD_ERR_ARG, "td_chain_create: prior must be 1 (uniform), 2 (normal) or 3 (exponential)");
     if (p.min_cells < 1 || p.max_cells < p.min_cells || p.sig <= 0 || p.zeta_scale <= 0)
         return set_err(ctx, TD_ERR_ARG, "td_chain_create: bad cell bounds / sig / zeta_scale");
     if (!(p.xmax >= p.xmin && p.ymax >= p.ymin && p.zmax >= p.zmin))
@@ -678,6 +698,7 @@ int tdt_accept(const td_chain_params *prm, int action, double u_accept, double z
     p.valid = 1;
     p.u_accept = u_accept;
     p.zeta = zeta_new;
+    if (action == tdchain::kBirth || action == tdchain::kChange) p.valid = tdchain::prior_valid(P, zeta_new);
     p.log_u = u_accept > 0.0 ? tdchain::det_log(u_accept) : -HUGE_VAL;
     double lnN[3];
     tdchain::log_window(lnN, ncells);

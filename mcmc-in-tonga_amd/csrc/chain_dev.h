@@ -46,6 +46,8 @@ struct ChainScalars {
     int ncells;            // cells in the model
     int nslots;            // slot high-water mark
     int nfree;             // free-slot stack depth
+    int last_action;       // Model.action / Model.accept of the last iteration (TD_inversion_function.jl:73-74,
+    int last_accept;       // 123,179,217,249): the proposal drawn and whether it was accepted
     int pad;
 };
 

@@ -653,6 +653,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     int cur_r = 0;
     bool pend_r = false;    // rays in HBM: an accepted proposal's chi^2 partial sums not yet written
     bool pend_sup = false;  // rays in HBM: its super-tiles' maxima not yet refreshed
+    int last_action = 0, last_accept = 0;  // tid 0: Model.action / accept of the last iteration
     for (long long it = 0; it < iters; ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
         if constexpr (WALK) {
@@ -1107,6 +1108,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 }
             }
         }
+        last_action = action;
+        last_accept = acc_r ? 1 : 0;
         STAMP(12);
         // ===== end of iteration: the next proposal (wave 0; draws refilled every 64) =====
         if (wv == 0) {
@@ -1178,6 +1181,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         s.ncells = sh.ncells;
         s.nslots = sh.nslots;
         s.nfree = sh.nfree;
+        if (iters > 0) {
+            s.last_action = last_action;
+            s.last_accept = last_accept;
+        }
         for (int k = 0; k < kProfSlots; ++k) s.prof[k] += sh.prof[k];
         s.prof[15] += sh.grid_fallbacks32;  // diagnostic: unproven grid searches
         if (d.st_host) *d.st_host = s;  // the host's pinned mirror: no copy back per chain

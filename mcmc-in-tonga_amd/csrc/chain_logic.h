@@ -1,5 +1,6 @@
 // chain_logic.h -- rj-MCMC proposal logic shared by the host chain and the
-// device-resident chain kernel (TD_inversion_function.jl:70-274, prior == 1).
+// device-resident chain kernel (TD_inversion_function.jl:70-274; priors 1
+// uniform, 2 normal, 3 exponential, define_TDstructure.jl:15).
 //
 // Everything here is __host__ __device__ and uses only IEEE +,-,*,/ and
 // sqrt (all correctly rounded on both sides, the TUs are compiled with
@@ -208,8 +209,11 @@ TD_HD double normal_quantile(double p) {
 // ------------------------------------------------------ the proposal ----
 enum Action : int { kBirth = 1, kDeath = 2, kChange = 3, kMove = 4 };
 
+enum Prior : int { kUniform = 1, kNormal = 2, kExponential = 3 };
+
 struct Params {
     int debug_prior, max_cells, min_cells;
+    int prior;                             // define_TDstructure.jl:15 (1 uniform, 2 normal, 3 exponential)
     double zeta_scale, sig_zeta;           // sig_zeta = zeta_scale*sig/100 (TD_inversion_function.jl:22)
     double xmin, xmax, ymin, ymax, zmin, zmax;
     double xr, yr, zr;                     // (sig/100)*(max-min), :30-32
@@ -219,12 +223,26 @@ struct Params {
     // the same numbers in both engines
     double log_prior_birth, log_prior_death;
     double inv_2t, inv_2sig2;
+    double inv_zs, inv_zs2, inv_2zs2;      // 1/zeta_scale, 1/zeta_scale^2, 1/(2 zeta_scale^2): priors 2, 3
 };
 
 // the derived constants of Params (after any change of temperature or sig_zeta)
 inline void params_derived(Params &P) {
     P.inv_2t = 1.0 / (2.0 * P.temperature);
     P.inv_2sig2 = 1.0 / (2.0 * P.sig_zeta * P.sig_zeta);
+    P.inv_zs = 1.0 / P.zeta_scale;
+    P.inv_zs2 = 1.0 / (P.zeta_scale * P.zeta_scale);
+    P.inv_2zs2 = 1.0 / (2.0 * (P.zeta_scale * P.zeta_scale));
+}
+
+// Is a proposed zeta inside the prior's support?  Birth (:92, :111) and change
+// (:195, :206): uniform (0, zeta_scale); normal: always (no check at :105-109,
+// :201-204); exponential: > 0.  (Death's exponential check is on the
+// Interpolation value at the killed site, :165: see accept().)
+TD_HD int prior_valid(const Params &P, double zeta) {
+    if (P.prior == kNormal) return 1;
+    if (P.prior == kExponential) return zeta > 0.0 ? 1 : 0;
+    return (zeta > 0.0 && zeta < P.zeta_scale) ? 1 : 0;
 }
 
 // What the iteration proposes, before any forward-model evaluation.
@@ -280,7 +298,7 @@ TD_HD void complete_proposal(const Params &P, const Draws &d, Proposal &p, doubl
     if (!p.active) return;
     if (p.action == kChange) {
         p.zeta = czeta + P.sig_zeta * d.z_zeta;
-        p.valid = (p.zeta > 0.0 && p.zeta < P.zeta_scale) ? 1 : 0;
+        p.valid = prior_valid(P, p.zeta);
     } else if (p.action == kMove) {
         p.x = cx + P.xr * d.z_a;
         p.y = cy + P.yr * d.z_b;
@@ -294,7 +312,7 @@ TD_HD void complete_proposal(const Params &P, const Draws &d, Proposal &p, doubl
 // Birth, once czeta = Interpolation(model, xNew, yNew, zNew) is known (:81-82, :92).
 TD_HD void birth_zeta(const Params &P, Proposal &p, double czeta) {
     p.zeta = czeta + P.sig_zeta * p.z_zeta;
-    p.valid = (p.zeta > 0.0 && p.zeta < P.zeta_scale) ? 1 : 0;
+    p.valid = prior_valid(P, p.zeta);
 }
 
 // {log(N-1), log(N), log(N+1)} for log_alpha (the device engine reads the same
@@ -303,34 +321,54 @@ inline void log_window(double out[3], int64_t N) {
     for (int k = 0; k < 3; ++k) out[k] = det_log((double)(N - 1 + k));
 }
 
-// The Metropolis-Hastings decision, prior == 1 (uniform): rand < min(1, alpha)
-// with alpha of eqs. 14-17 (TD_inversion_function.jl:96-97 birth, :151-152
-// death, :196 change, :241 move), decided in the log domain:
-//     log u < log alpha = log f + g + (phi - phi_n)/(2T)
+// The Metropolis-Hastings decision: rand < min(1, alpha) with alpha of
+// eqs. 14-17, decided in the log domain:
+//     log u < log alpha = log f + h + (phi - phi_n)/(2T)
 // (u < 1, so the min(1, .) never matters; the same decision as comparing u
-// with alpha, without an exp on the critical path).  lnN = {log(N-1), log N,
-// log(N+1)} (det_log), so the model-size factor is lnN[1] - lnN[1 +- 1].
-// extra: birth -> czeta, death -> zetanew = Interpolation(modeln, killed site) (:146)
+// with alpha, without an exp on the critical path).  log f = the model-size
+// factor lnN[1] - lnN[1 +- 1] (det_log) plus the constant prior ratio (host
+// libm log); h = the exponent's zeta terms, per prior:
+//   birth  (:96-97 / :107-108 / :113-114, eq. 16), dz = czeta - zetanew:
+//     uniform dz^2/2s^2, normal -zn^2/zs^2 + dz^2/2s^2 (zs^2, not 2 zs^2, as
+//     the reference writes it), exponential -zn/zs + dz^2/2s^2
+//   death  (:151-152 / :160-162 / :166-168, eq. 17), dz = zeta_killed -
+//     zetanew, zetanew = Interpolation(modeln, killed site) (:146):
+//     uniform -dz^2/2s^2, normal zk^2/2zs^2 - dz^2/2s^2, exponential zk/zs - dz^2/2s^2
+//   change (:196 / :202-203 / :207-208, eq. 15), zo = the old value (passed
+//     as zeta_killed): uniform 0, normal (zo^2 - zn^2)/2zs^2, exponential (zo - zn)/zs
+//   move   (:241, eq. 14): 0.
+// T = 1 is the reference; a tempered replica divides only the misfit term.
 // Written as one if-chain into one variable: a `switch` with a `return -x`
 // default was miscompiled for gfx950 (the default path returned a stale
 // register; tools/repro_accept.hip).
 TD_HD double log_alpha(const Params &P, const Proposal &p, double phi, double phi_n, double czeta,
                        double zeta_killed, double zetanew_death, const double *lnN) {
-    // (multiplications by precomputed 1/(2T), 1/(2 sig^2): no division on the device's decision path)
-    const double g = (phi - phi_n) * P.inv_2t;  // change eq. 15 (:196), move eq. 14 (:241)
+    // (multiplications by precomputed reciprocals: no division on the device's decision path)
+    const double g = (phi - phi_n) * P.inv_2t;
     double la = g;
-    if (p.action == kBirth) {  // eq. 16, :96-97: (N/(N+1)) (sig_zeta sqrt(2 pi) / zeta_scale) exp(dz^2/(2 sig^2) - dphi)
+    if (p.action == kBirth) {
         const double dz = czeta - p.zeta;
-        la = ((lnN[1] - lnN[2]) + P.log_prior_birth) + ((dz * dz) * P.inv_2sig2 + g);
-    } else if (p.action == kDeath) {  // eq. 17, :151-152: (N/(N-1)) (zeta_scale / (sig_zeta sqrt(2 pi))) exp(-dz^2/(2 sig^2) - dphi)
+        double h = (dz * dz) * P.inv_2sig2;
+        if (P.prior == kNormal) h = -(p.zeta * p.zeta) * P.inv_zs2 + h;
+        else if (P.prior == kExponential) h = -p.zeta * P.inv_zs + h;
+        la = ((lnN[1] - lnN[2]) + P.log_prior_birth) + (h + g);
+    } else if (p.action == kDeath) {
         const double dz = zeta_killed - zetanew_death;
-        la = ((lnN[1] - lnN[0]) + P.log_prior_death) + (g - (dz * dz) * P.inv_2sig2);
+        double h = -((dz * dz) * P.inv_2sig2);
+        if (P.prior == kNormal) h = (zeta_killed * zeta_killed) * P.inv_2zs2 + h;
+        else if (P.prior == kExponential) h = zeta_killed * P.inv_zs + h;
+        la = ((lnN[1] - lnN[0]) + P.log_prior_death) + (h + g);
+    } else if (p.action == kChange) {
+        if (P.prior == kNormal) la = (zeta_killed * zeta_killed - p.zeta * p.zeta) * P.inv_2zs2 + g;
+        else if (P.prior == kExponential) la = (zeta_killed - p.zeta) * P.inv_zs + g;
     }
     return la;
 }
 TD_HD bool accept(const Params &P, const Proposal &p, double phi, double phi_n, double czeta, double zeta_killed,
                   double zetanew_death, const double *lnN) {
     if (!p.active || !p.valid) return false;  // rand(1)[1] < alpha && valid == 1
+    // exponential death: valid only when the reduced model's value at the killed site is > 0 (:165, :171)
+    if (p.action == kDeath && P.prior == kExponential && !(zetanew_death > 0.0)) return false;
     return p.log_u < log_alpha(P, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN);
 }
 

@@ -134,6 +134,76 @@ def load(path):
             return unpack({k: z[k] for k in z.files})
 
 
+# DataStruct fields in DefStruct.jl:5-30 order (jld_h5.py keeps the same list: it
+# runs standalone under the h5py interpreter)
+DS_FIELDS = ["tS", "allaveatten", "allLats", "allLons", "allSig", "dataX", "dataY", "xVec", "yVec", "zVec",
+             "elonsX", "elatsY", "elons", "elats", "edep", "coastX", "coastY", "rayX", "rayY", "rayZ", "rayL",
+             "rayU", "U"]
+DS_RANGES = ("xVec", "yVec", "zVec")
+
+
+def _range_triple(v):
+    v = np.asarray(v, dtype=np.float64).ravel()
+    step = float(v[1] - v[0]) if len(v) > 1 else 0.0
+    return np.array([float(v[0]) if len(v) else 0.0, step, float(len(v))])
+
+
+def save_checkpoint(path, model, dataStruct, it, burnin, model_hist=(), saved=0, model_num=0):  # noqa: N803
+    """A chain checkpoint with the fields of TD_inversion_function.jl:285
+    (burnin = True: model, dataStruct, iter, saved_#, model_num, model_hist)
+    or :292 (burnin = False: model, dataStruct, iter)."""
+    p = pack([[model], list(model_hist) if burnin else []])
+    p["ck_iter"] = np.array(float(it))
+    p["ck_iter_int"] = np.array(0 if burnin else 1)  # :285 iter (Float64 loop variable), :292 Int64(iter)
+    p["ck_burnin"] = np.array(1 if burnin else 0)
+    p["ck_saved"] = np.array(int(saved))
+    p["ck_model_num"] = np.array(int(model_num))
+    for fld in DS_FIELDS:
+        v = getattr(dataStruct, fld)
+        if fld in DS_RANGES:
+            p["ds_" + fld + "_range"] = _range_triple(v)
+        else:
+            p["ds_" + fld] = np.asarray(v, dtype=np.float64)
+    _write_packed(path, p, "write_checkpoint")
+
+
+def load_checkpoint(path):
+    """The checkpoint entries TD_inversion_function.jl:56-66 reads back:
+    dict(model, iter, burnin, model_hist, saved, model_num, ds) -- model_hist,
+    saved, model_num only when burnin (as the reference)."""
+    p = _read_packed(path, "read_checkpoint")
+    chains = unpack(p)
+    out = {"model": chains[0][0], "iter": float(p["ck_iter"]), "iter_is_int": bool(int(p["ck_iter_int"])),
+           "burnin": bool(int(p["ck_burnin"])), "model_hist": chains[1] if len(chains) > 1 else [],
+           "ds": {k[3:]: p[k] for k in p if k.startswith("ds_")}}
+    if out["burnin"]:
+        out["saved"] = int(p["ck_saved"])
+        out["model_num"] = int(p["ck_model_num"])
+    return out
+
+
+def _write_packed(path, p, cmd):
+    py, path = h5py_python(), os.path.abspath(path)
+    if py is None:
+        getattr(_module(), cmd)(path, p)
+        return
+    with tempfile.TemporaryDirectory() as td:
+        tmp = os.path.join(td, "packed.npz")
+        np.savez(tmp, **p)
+        _subprocess(py, [cmd, tmp, path])
+
+
+def _read_packed(path, cmd):
+    py, path = h5py_python(), os.path.abspath(path)
+    if py is None:
+        return getattr(_module(), cmd)(path)
+    with tempfile.TemporaryDirectory() as td:
+        tmp = os.path.join(td, "packed.npz")
+        _subprocess(py, [cmd, path, tmp])
+        with np.load(tmp, allow_pickle=False) as z:
+            return {k: z[k] for k in z.files}
+
+
 def fingerprint(path):
     """jld_h5.fingerprint: the file's HDF5 structure as nested lists (JSON types)."""
     import json

@@ -26,6 +26,8 @@ from the files it reads.
 
 usage: python jld_h5.py write PACKED.npz OUT.jld
        python jld_h5.py read IN.jld PACKED.npz
+       python jld_h5.py write_checkpoint PACKED.npz OUT.jld
+       python jld_h5.py read_checkpoint IN.jld PACKED.npz
 """
 import sys
 
@@ -165,6 +167,197 @@ def write(path, packed, julia_version=(1, 5, 2)):
         fh.write(HEADER + b"\0" * (USERBLOCK - len(HEADER)))
 
 
+# ---------------------------------------------------------------- checkpoints ----
+# TD_inversion_function.jl:285 / :292 save(modelname, "model", m, "dataStruct", d, "iter", iter,
+# ["saved_#", n, "model_num", k, "model_hist", hist,] "burnin", b).  Model records and the
+# Vector{Any} of models follow model.jld's layout (pinned by the reference file); the rest
+# (DataStruct's committed compound, StepRangeLen / TwicePrecision members, Bool) follows JLD
+# 0.1.3's conventions without a reference file to pin it (no checkpoint ships).
+DS_FIELDS = ["tS", "allaveatten", "allLats", "allLons", "allSig", "dataX", "dataY", "xVec", "yVec", "zVec",
+             "elonsX", "elatsY", "elons", "elats", "edep", "coastX", "coastY", "rayX", "rayY", "rayZ", "rayL",
+             "rayU", "U"]
+DS_RANGES = ("xVec", "yVec", "zVec")
+DS_MATRICES = ("elonsX", "elatsY", "elons", "elats", "edep", "coastX", "coastY", "rayX", "rayY", "rayZ", "rayL",
+               "rayU", "U")
+
+
+def _twice_type():
+    t = h5t.create(h5t.COMPOUND, 16)
+    t.insert(b"hi_", 0, h5t.IEEE_F64LE)
+    t.insert(b"lo_", 8, h5t.IEEE_F64LE)
+    return t
+
+
+def _range_raw_dtype():
+    tw = np.dtype([("hi_", "<f8"), ("lo_", "<f8")])
+    return np.dtype([("ref_", tw), ("step_", tw), ("len_", "<i8"), ("offset_", "<i8")])
+
+
+def write_checkpoint(path, packed, julia_version=(1, 5, 2)):
+    """One chain checkpoint.  packed: jld.pack([[model], model_hist]) plus
+    ck_* scalars and ds_* DataStruct arrays (see jld.save_checkpoint)."""
+    f = h5py.File(path, "w", userblock_size=USERBLOCK, libver="earliest")
+    fid = f.id
+    for g in ("_creator", "_refs", "_types"):
+        h5g.create(fid, g.encode())
+    _dataset(fid, "_creator/ENDIAN_BOM", np.array(0x04030201, dtype="<u4"))
+    for k, v in zip(("JULIA_MAJOR", "JULIA_MINOR", "JULIA_PATCH"), julia_version):
+        _dataset(fid, "_creator/" + k, np.array(v, dtype="<u4"))
+    _dataset(fid, "_creator/WORD_SIZE", np.array(64, dtype="<i8"))
+    refs = _Refs()
+    mtid = model_type()
+    mtid.commit(fid, b"_types/00000001")
+    _str_attr(mtid, "julia type", "Model")
+    raw = model_raw_dtype()
+    written = {}
+
+    def model_record(j, name):
+        arrays = {}
+        for fld in ARRAY_FIELDS:
+            key = fld[:-1]
+            off = packed[key + "_off"]
+            a = np.ascontiguousarray(packed[key][int(off[j]):int(off[j + 1])], dtype="<f8")
+            nm = refs.next()
+            _dataset(fid, nm, a)
+            arrays[fld] = _ref(fid, nm)
+        rec = np.zeros((), dtype=raw)
+        for k in ("nCells", "phi", "likelihood", "action", "accept", "zeta_xz", "zeta_xy"):
+            rec[k + "_"] = packed[k][j]
+        for fld, r in arrays.items():
+            rec[fld] = r
+        _dataset(fid, name, rec, ftype=mtid, mtype=mtid)
+        written[j] = _ref(fid, name)
+
+    entry, co = packed["entry"], packed["chain_off"]
+    model_record(int(entry[0]), "model")  # "model", CurrentModel
+    # "dataStruct": committed compound; arrays by reference, ranges inline (isbits)
+    tw = _twice_type()
+    tw.commit(fid, b"_types/00000002")
+    _str_attr(tw, "julia type", "Base.TwicePrecision{Core.Float64}")
+    rr = _range_raw_dtype()
+    rt = h5t.create(h5t.COMPOUND, rr.itemsize)
+    rt.insert(b"ref_", 0, tw)
+    rt.insert(b"step_", 16, tw)
+    rt.insert(b"len_", 32, h5t.STD_I64LE)
+    rt.insert(b"offset_", 40, h5t.STD_I64LE)
+    rt.commit(fid, b"_types/00000003")
+    _str_attr(rt, "julia type", "Base.StepRangeLen{Core.Float64,Base.TwicePrecision{Core.Float64},"
+                                "Base.TwicePrecision{Core.Float64}}")
+    members, off = [], 0
+    for fld in DS_FIELDS:
+        size = rr.itemsize if fld in DS_RANGES else 8
+        members.append((fld, off, size))
+        off += size
+    dt = h5t.create(h5t.COMPOUND, off)
+    for fld, o, _ in members:
+        dt.insert((fld + "_").encode(), o, rt if fld in DS_RANGES else h5t.STD_REF_OBJ)
+    dt.commit(fid, b"_types/00000004")
+    _str_attr(dt, "julia type", "DataStruct")
+    rec = np.zeros(off, dtype=np.uint8)
+    for fld, o, size in members:
+        if fld in DS_RANGES:
+            first, step, n = packed["ds_" + fld + "_range"]
+            r = np.zeros((), dtype=rr)
+            r["ref_"]["hi_"], r["step_"]["hi_"], r["len_"], r["offset_"] = first, step, int(n), 1
+            rec[o:o + size] = np.frombuffer(r.tobytes(), dtype=np.uint8)
+        else:
+            a = np.asarray(packed["ds_" + fld], dtype="<f8")
+            if fld in DS_MATRICES:  # Julia m x n column-major == HDF5 (n, m)
+                a = a.reshape(-1, 1) if a.ndim == 1 else a
+                a = np.ascontiguousarray(a.T)
+            nm = refs.next()
+            _dataset(fid, nm, a)
+            rec[o:o + 8] = np.frombuffer(np.array(_ref(fid, nm), dtype="<u8").tobytes(), dtype=np.uint8)
+    space = h5s.create(h5s.SCALAR)
+    dcpl = h5p.create(h5p.DATASET_CREATE)
+    dcpl.set_layout(h5d.COMPACT)
+    did = h5d.create(fid, b"dataStruct", dt, space, dcpl=dcpl)
+    did.write(h5s.ALL, h5s.ALL, rec, mtype=dt)
+    # "iter": Float64 after burn-in (the loop variable of 1:n_iter), Int64 before (:292 Int64(iter))
+    if int(packed["ck_iter_int"]):
+        _dataset(fid, "iter", np.array(int(packed["ck_iter"]), dtype="<i8"))
+    else:
+        _dataset(fid, "iter", np.array(float(packed["ck_iter"]), dtype="<f8"))
+    burnin = bool(int(packed["ck_burnin"]))
+    if burnin:
+        _dataset(fid, "saved_#", np.array(int(packed["ck_saved"]), dtype="<i8"))
+        _dataset(fid, "model_num", np.array(int(packed["ck_model_num"]), dtype="<i8"))
+        model_refs = []
+        for e in range(int(co[1]), int(co[2])):
+            j = int(entry[e])
+            if j not in written:
+                model_record(j, refs.next())
+            model_refs.append(written[j])
+        arr = np.array(model_refs, dtype="<u8").reshape(len(model_refs))
+        did = _dataset(fid, "model_hist", arr, ftype=h5t.STD_REF_OBJ, mtype=h5t.STD_REF_OBJ)
+        _str_attr(did, "julia eltype", "Core.Any")
+    did = _dataset(fid, "burnin", np.array(1 if burnin else 0, dtype="u1"))
+    _str_attr(did, "julia type", "Core.Bool")
+    f.close()
+    with open(path, "r+b") as fh:
+        fh.write(HEADER + b"\0" * (USERBLOCK - len(HEADER)))
+
+
+def read_checkpoint(path):
+    """The entries TD_inversion_function.jl:56-66 reads back, packed like
+    write_checkpoint's input (model = chain 0, model_hist = chain 1)."""
+    f = h5py.File(path, "r")
+    mdt = model_dtype()
+    mt = h5t.py_create(mdt)
+    cols = {k: [] for k in ("nCells", "phi", "likelihood", "action", "accept", "zeta_xz", "zeta_xy")}
+    arrays = {fld[:-1]: [] for fld in ARRAY_FIELDS}
+    stored, entry = {}, []
+
+    def take(d):
+        key = h5o.get_info(d.id).addr
+        if key not in stored:
+            stored[key] = len(stored)
+            a = np.empty((), dtype=mdt)
+            d.id.read(h5s.ALL, h5s.ALL, a, mtype=mt)
+            for k in cols:
+                cols[k].append(a[k + "_"][()])
+            for fld in ARRAY_FIELDS:
+                arrays[fld[:-1]].append(np.asarray(f[a[fld][()]][()], dtype=np.float64).ravel())
+        entry.append(stored[key])
+
+    take(f["model"])
+    chain_off = [0, 1]
+    burnin = bool(f["burnin"][()])
+    out = {}
+    if burnin:
+        hist = f["model_hist"]
+        for j in range(hist.shape[0]):
+            take(f[hist[j]])
+        out["ck_saved"] = np.array(int(f["saved_#"][()]))
+        out["ck_model_num"] = np.array(int(f["model_num"][()]))
+    chain_off.append(len(entry))
+    it = f["iter"]
+    out["ck_iter"] = np.array(float(it[()]))
+    out["ck_iter_int"] = np.array(1 if it.dtype.kind == "i" else 0)
+    out["ck_burnin"] = np.array(1 if burnin else 0)
+    out["chain_off"] = np.array(chain_off, dtype=np.int64)
+    out["entry"] = np.array(entry, dtype=np.int64)
+    for k, v in cols.items():
+        out[k] = np.array(v, dtype=np.int64 if k in ("action", "accept") else np.float64)
+    for k, v in arrays.items():
+        out[k] = np.concatenate(v) if v else np.zeros(0)
+        out[k + "_off"] = np.concatenate([[0], np.cumsum([len(a) for a in v])]).astype(np.int64)
+    ds = f["dataStruct"]
+    rr = _range_raw_dtype()
+    ddt = np.dtype([(fld + "_", rr if fld in DS_RANGES else h5py.ref_dtype) for fld in DS_FIELDS])
+    rec = np.empty((), dtype=ddt)
+    ds.id.read(h5s.ALL, h5s.ALL, rec, mtype=h5t.py_create(ddt))
+    for fld in DS_FIELDS:
+        v = rec[fld + "_"][()]
+        if fld in DS_RANGES:
+            out["ds_" + fld + "_range"] = np.array([v["ref_"]["hi_"], v["step_"]["hi_"], v["len_"]], dtype=np.float64)
+        else:
+            a = np.asarray(f[v][()], dtype=np.float64)
+            out["ds_" + fld] = np.ascontiguousarray(a.T) if fld in DS_MATRICES else a
+    f.close()
+    return out
+
+
 def read(path):
     """The ``model`` entry of a JLD file (a vector of chains of Models), packed."""
     f = h5py.File(path, "r")
@@ -254,6 +447,11 @@ def main(argv):
             write(argv[3], {k: z[k] for k in z.files})
     elif len(argv) == 4 and argv[1] == "read":
         np.savez(argv[3], **read(argv[2]))
+    elif len(argv) == 4 and argv[1] == "write_checkpoint":
+        with np.load(argv[2], allow_pickle=False) as z:
+            write_checkpoint(argv[3], {k: z[k] for k in z.files})
+    elif len(argv) == 4 and argv[1] == "read_checkpoint":
+        np.savez(argv[3], **read_checkpoint(argv[2]))
     elif len(argv) == 3 and argv[1] == "fingerprint":
         import json
         print(json.dumps(fingerprint(argv[2])))

@@ -120,7 +120,7 @@ def test_normal_quantile(tt):
 
 
 def params(tt, **kw):
-    prm = tt.define_TDstructrure().replace(**{k: v for k, v in kw.items() if k in ("max_cells", "min_cells",
+    prm = tt.define_TDstructrure().replace(**{k: v for k, v in kw.items() if k in ("max_cells", "min_cells", "prior",
                                                                                     "debug_prior")})
     return tt.chain_params(prm, None, seed=kw.get("seed", 3), chain=kw.get("chain", 1),
                            temperature=kw.get("temperature", 1.0))
@@ -181,16 +181,67 @@ def test_proposals_follow_reference_branches(tt):
             assert active == 0
 
 
-def alpha_reference(action, N, phi, phi_n, czeta=0.0, zetanew=0.0, zeta_killed=0.0, zdn=0.0, T=1.0):
-    """TD_inversion_function.jl eqs. 14-17 (prior 1), restated in Python."""
+@pytest.mark.parametrize("prior", [2, 3])
+def test_proposal_validity_per_prior(tt, prior):
+    """Birth/change zeta validity: normal -- always (:105-109, :201-204);
+    exponential -- zeta > 0 (:111, :206)."""
+    prm = params(tt, max_cells=100, min_cells=5, prior=prior)
+    model = tt.random_model(40, 4)
+    model.zeta[:] = 1.0  # near 0: changes often step below it
+    n_invalid = 0
+    for it in range(1, 3000):
+        a, active, valid, idx, x, y, z, zeta = propose(tt, prm, it, model.cells(), czeta_birth=1.0)
+        if int(a) in (1, 3):
+            assert valid == (1 if prior == 2 else int(zeta > 0))
+            n_invalid += valid == 0
+    assert (n_invalid == 0) == (prior == 2)
+
+
+def alpha_reference(action, N, phi, phi_n, czeta=0.0, zetanew=0.0, zeta_killed=0.0, zdn=0.0, T=1.0, prior=1):
+    """TD_inversion_function.jl eqs. 14-17, restated in Python for the three
+    priors (uniform :96-97,151-152,196; normal :107-108,160-162,202-203;
+    exponential :113-114,166-168,207-208); 0 where the reference sets valid = 0
+    or alpha = 0.  For change, zetanew is the new value, zeta_killed the old."""
     sig_zeta, zs = 50 * 10 / 100, 50
     d = (phi_n - phi) / (2 * T)
+    s2p = math.sqrt(2 * math.pi)
     if action == 1:
-        a = (N / (N + 1)) * ((sig_zeta * math.sqrt(2 * math.pi)) / zs) * \
-            math.exp(((czeta - zetanew) ** 2) / (2 * sig_zeta ** 2) - d)
+        if prior == 1:
+            if not (0 < zetanew < zs):
+                return 0.0
+            a = (N / (N + 1)) * ((sig_zeta * s2p) / zs) * math.exp(((czeta - zetanew) ** 2) / (2 * sig_zeta ** 2) - d)
+        elif prior == 2:
+            a = (N / (N + 1)) * (sig_zeta / zs) * \
+                math.exp(-zetanew ** 2 / zs ** 2 + (czeta - zetanew) ** 2 / (2 * sig_zeta ** 2) - d)
+        else:
+            if not zetanew > 0:
+                return 0.0
+            a = (N / (N + 1)) * (s2p * sig_zeta / zs) * \
+                math.exp(-zetanew / zs + (czeta - zetanew) ** 2 / (2 * sig_zeta ** 2) - d)
     elif action == 2:
-        a = (N / (N - 1)) * (zs / (sig_zeta * math.sqrt(2 * math.pi))) * \
-            math.exp(-((zeta_killed - zdn) ** 2) / (2 * sig_zeta ** 2) - d)
+        zk = zeta_killed
+        if prior == 1:
+            a = (N / (N - 1)) * (zs / (sig_zeta * s2p)) * math.exp(-((zk - zdn) ** 2) / (2 * sig_zeta ** 2) - d)
+        elif prior == 2:
+            a = (N / (N - 1)) * (zs / sig_zeta) * \
+                math.exp(zk ** 2 / (2 * zs ** 2) - (zk - zdn) ** 2 / (2 * sig_zeta ** 2) - d)
+        else:
+            if not zdn > 0:
+                return 0.0
+            a = (N / (N - 1)) * (zs / (s2p * sig_zeta)) * \
+                math.exp(zk / zs - (zk - zdn) ** 2 / (2 * sig_zeta ** 2) - d)
+    elif action == 3:
+        zo = zeta_killed
+        if prior == 1:
+            if not (0 < zetanew < zs):
+                return 0.0
+            a = math.exp(-d)
+        elif prior == 2:
+            a = math.exp((zo ** 2 - zetanew ** 2) / (2 * zs ** 2) - d)
+        else:
+            if not zetanew > 0:
+                return 0.0
+            a = math.exp((zo - zetanew) / zs - d)
     else:
         a = math.exp(-d)
     return min(1.0, a)
@@ -199,17 +250,18 @@ def alpha_reference(action, N, phi, phi_n, czeta=0.0, zetanew=0.0, zeta_killed=0
 def test_acceptance_matches_reference_formulas(tt):
     L = tt.lib()
     rng = np.random.default_rng(7)
-    for T in (1.0, 3.0):
-        prm = params(tt, temperature=T)
-        for _ in range(4000):
-            action = int(rng.integers(1, 5))
-            N = int(rng.integers(6, 99))
-            phi = rng.uniform(100, 900)
-            phi_n = phi + rng.normal(0, 6)
-            cz, zn, zk, zd = rng.uniform(0, 50, 4)
-            a = alpha_reference(action, N, phi, phi_n, cz, zn, zk, zd, T)
-            u = rng.uniform()
-            if abs(u - a) < 1e-12:
-                continue
-            got = L.tdt_accept(ctypes.byref(prm), action, u, zn, N, phi, phi_n, cz, zk, zd)
-            assert got == (1 if u < a else 0)
+    for prior in (1, 2, 3):
+        for T in (1.0, 3.0):
+            prm = params(tt, temperature=T, prior=prior)
+            for _ in range(3000):
+                action = int(rng.integers(1, 5))
+                N = int(rng.integers(6, 99))
+                phi = rng.uniform(100, 900)
+                phi_n = phi + rng.normal(0, 6)
+                cz, zn, zk, zd = rng.uniform(-10, 60, 4) if prior != 1 else rng.uniform(0, 50, 4)
+                a = alpha_reference(action, N, phi, phi_n, cz, zn, zk, zd, T, prior)
+                u = rng.uniform()
+                if abs(u - a) < 1e-12:
+                    continue
+                got = L.tdt_accept(ctypes.byref(prm), action, u, zn, N, phi, phi_n, cz, zk, zd)
+                assert got == (1 if u < a else 0), (prior, action, a, u)

@@ -238,3 +238,33 @@ def test_stress_geometry_chain_follows_host_engine(tt):
     dev.close()
     host.close()
     ctx.close()
+
+
+@pytest.mark.parametrize("prior,ncells,iters,seed", [(2, 300, 400, 71), (3, 300, 400, 72), (2, 2000, 200, 73),
+                                                     (3, 1000, 200, 74), (2, 0, 400, 75), (3, 0, 400, 76)])
+def test_priors_device_follows_host(tt, ds, ctx, prior, ncells, iters, seed):
+    """Normal (2) and exponential (3) priors (TD_inversion_function.jl:105-119,
+    157-172, 201-212; start MCsub.jl:102-107 when ncells = 0): the device
+    engine makes the host engine's decisions bit for bit."""
+    prm = tt.define_TDstructrure().replace(prior=prior, max_cells=max(ncells, 100) + 200)
+    model = tt.random_model(ncells, seed) if ncells else None
+    if model is not None and prior == 2:
+        model.zeta[:] = np.random.default_rng(seed).normal(0.0, 50.0, ncells)  # the normal prior's start
+    dev = make(tt, ctx, prm, model, seed, tt.TD_ENGINE_DEVICE)
+    host = make(tt, ctx, prm, model, seed, tt.TD_ENGINE_HOST)
+    m0 = dev.model()
+    if ncells == 0:  # build_starting drew the same model in both engines
+        assert same_models(m0, host.model())
+        if prior == 3:
+            assert np.all(m0.zeta > 0)
+    for _ in range(4):
+        dev.run(iters // 4)
+        host.run(iters // 4)
+        sd, sh = dev.stats(), host.stats()
+        assert sd["phi"] == sh["phi"], (sd, sh)
+        assert sd["accepted"] == sh["accepted"] and sd["proposed"] == sh["proposed"]
+    assert same_models(dev.model(), host.model())
+    assert sum(sd["accepted"]) > 0
+    m = dev.model()
+    ptS, phi, _, _ = ctx.evaluate(m.cells())
+    assert phi == m.phi and np.array_equal(ptS, m.ptS)

@@ -93,3 +93,39 @@ def test_own_models_and_large_arrays(tt, jld, tmp_path):
         for a, b in zip(ca, cb):
             assert np.array_equal(a.xCell, b.xCell) and np.array_equal(a.zeta, b.zeta)
             assert np.array_equal(a.ptS, b.ptS) and a.phi == b.phi and a.action == b.action
+
+
+def test_checkpoint_round_trip(tt, ds, jld, tmp_path):
+    """A chain checkpoint (TD_inversion_function.jl:285 burn-in / :292 before):
+    the model, model_hist (aliasing kept), iter, saved_#, model_num, burnin and
+    the DataStruct arrays come back bit for bit."""
+    rng = np.random.default_rng(4)
+    hist = []
+    for k in range(4):
+        m = tt.random_model(int(rng.integers(5, 40)), k)
+        m.phi, m.ptS, m.tS, m.likelihood = float(rng.uniform(10, 99)), rng.random(len(ds.tS)), ds.tS, 3.25
+        m.action, m.accept = int(rng.integers(1, 5)), int(rng.integers(0, 2))
+        hist.append(m)
+    hist.append(hist[-1])  # the reference pushes the same object when nothing was accepted in between
+    path = tmp_path / "chain3_iter777_77.7%.jld"
+    jld.save_checkpoint(path, hist[-1], ds, 777.0, True, hist, saved=5, model_num=100)
+    c = jld.load_checkpoint(path)
+    assert c["burnin"] and c["iter"] == 777.0 and c["saved"] == 5 and c["model_num"] == 100
+    assert len(c["model_hist"]) == 5 and c["model_hist"][3] is c["model_hist"][4] is c["model"]
+    for a, b in zip(c["model_hist"], hist):
+        for f in ("xCell", "yCell", "zCell", "zeta", "ptS", "tS"):
+            assert np.array_equal(getattr(a, f), getattr(b, f))
+        assert (a.phi, a.likelihood, a.action, a.accept, a.nCells) == (b.phi, b.likelihood, b.action, b.accept,
+                                                                      b.nCells)
+    for f in ("tS", "allSig", "rayX", "rayY", "rayZ", "rayL", "rayU", "U"):
+        assert np.array_equal(c["ds"][f], getattr(ds, f), equal_nan=True), f
+    assert list(c["ds"]["xVec_range"]) == [ds.xVec[0], ds.xVec[1] - ds.xVec[0], len(ds.xVec)]
+    pre = tmp_path / "chain3_iter100_10%.jld"
+    jld.save_checkpoint(pre, hist[0], ds, 100, False)
+    p = jld.load_checkpoint(pre)
+    assert not p["burnin"] and p["iter_is_int"] and p["iter"] == 100 and p["model_hist"] == []
+    assert "saved" not in p
+    fp = jld.fingerprint(path)
+    assert fp[0] == ["userblock", "Julia data file (HDF5), version 0.1.3"]
+    top = {e[0] for e in fp if "/" not in e[0]}
+    assert {"model", "dataStruct", "iter", "saved_#", "model_num", "model_hist", "burnin"} <= top
