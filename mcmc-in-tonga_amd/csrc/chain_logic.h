@@ -48,11 +48,13 @@ TD_HD U4 philox(U4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-// 53-bit uniform in (0,1): (k + 0.5) / 2^53, never 0 or 1.
+// Uniform in (0,1): (k + 0.5) / 2^52 for a 52-bit k -- k + 0.5 is exact in
+// FP64, so u lies in [2^-53, 1 - 2^-53], never 0 or 1 (with a 53-bit k the
+// sum rounds to 2^53 for the top values: u = 1 and an infinite normal
+// quantile; found by the host sanitizer driver, oracle/san).
 TD_HD double u01(uint32_t a, uint32_t b) {
-    const uint64_t k = ((uint64_t)a << 21) ^ (uint64_t)(b >> 11);
-    const uint64_t m = k & ((1ull << 53) - 1);
-    return ((double)m + 0.5) * (1.0 / 9007199254740992.0);
+    const uint64_t k = (((uint64_t)a << 20) ^ (uint64_t)(b >> 12)) & ((1ull << 52) - 1);
+    return ((double)k + 0.5) * (1.0 / 4503599627370496.0);
 }
 
 // Draw slots of one iteration: each slot is one Philox block = 2 uniforms.
