@@ -45,15 +45,56 @@ FP64_NOFMA_PEAK_TFLOPS = FP64_VALU_PEAK_TFLOPS / 2
 
 
 def measured_traffic(key):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes of this
-    same command (profiles/traffic.json, written from tools/profile.sh
-    output: FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or None."""
+    """HBM bytes per launch from the committed rocprofv3 PMC passes
+    (profiles/traffic.json, written by profiles/make_traffic.py from
+    tools/profile.sh output: FETCH_SIZE x2 + WRITE_SIZE per
+    MI355X_MICROARCH.md) and that profile's kernel-trace average launch time;
+    (None, None, None) when absent.  Not measured in this run."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             t = json.load(f)[key]
-        return round(float(t["traffic_bytes_per_launch"]), 1), t["source"]
+        return round(float(t["traffic_bytes_per_launch"]), 1), t["source"], t.get("avg_launch_us")
     except (OSError, KeyError, ValueError):
-        return None, None
+        return None, None, None
+
+
+def model_bytes(P, n, N):
+    """SURVEY 8(d)'s algorithmic (compulsory) bytes of one full evaluate:
+    24 P (points) + 8 S (w = l*u per segment) + 32 N (cells) + 24 n (tS, sigma,
+    ptS), S = P - n segments.  The chain's proposals are evaluated
+    incrementally, so this is the byte count the reference's structure needs
+    per proposal, not what the incremental kernel reads."""
+    S = P - n
+    return 24 * P + 8 * S + 32 * N + 24 * n
+
+
+def chain_roofline(kernel, bytes_per_proposal, proposals_per_launch, avg_launch_s, counted_bytes_per_launch,
+                   traffic_key, match):
+    """roofline block of a chain kernel: `achieved` = SURVEY 8(d) model bytes
+    per launch / the launch's HIP-event time; beside it the fraction by the
+    kernel's own in-kernel byte count and by the PMC-measured HBM traffic
+    (committed profile of the same command, `traffic_source`)."""
+    per_launch = bytes_per_proposal * proposals_per_launch
+    achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    out = {"kernel": kernel, "bound": "hbm", "limiter": "latency: one persistent workgroup per chain (dependent "
+                                                        "barriers and L2/LDS round trips), DESIGN.md 4.2",
+           "bytes_model": "SURVEY 8(d) 24P+8S+32N+24n = %d B per proposal" % bytes_per_proposal,
+           "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None, "traffic_source": None,
+           "traffic_measured_in_this_run": False, "algorithmic_bytes_per_launch": round(per_launch, 1),
+           "proposals_per_launch": proposals_per_launch, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+           "us_per_proposal": round(avg_launch_s / max(proposals_per_launch, 1) * 1e6, 4),
+           "in_kernel_bytes_per_launch": round(counted_bytes_per_launch, 1),
+           "frac_in_kernel_count": round(counted_bytes_per_launch / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6)
+           if avg_launch_s > 0 else 0.0}
+    if match:
+        tr, src, prof_us = measured_traffic(traffic_key)
+        if tr is not None:
+            out["traffic"], out["traffic_source"] = tr, src
+            out["frac_measured_traffic"] = round(tr / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6)
+            if prof_us:
+                out["profile_avg_launch_ms"] = round(prof_us / 1e3, 4)
+    return out
 
 
 def parse():
@@ -175,7 +216,6 @@ def main():
         launches = max(launches, 1)
     bytes_per_launch = nbytes / max(launches, 1)
     avg_s = kms / 1e3 / max(launches, 1)
-    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
     out = {
         "metric": "MCMC proposals/sec (likelihood evals/sec) at 381 rays x N cells",
         "value": round(value, 1),
@@ -199,15 +239,10 @@ def main():
         "nn_pair_evals_per_s_equiv": round(value * P * N, 1),
         "acceptance": {"birth/death/change/move accepted": acc, "proposed": prop,
                        "rate": round(sum(acc) / max(sum(prop), 1), 4)},
-        "roofline": {"kernel": "k_chain_run", "bound": "hbm", "achieved": round(achieved, 3),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": None, "traffic_source": None,
-                     "algorithmic_bytes_per_launch": round(bytes_per_launch, 1),
-                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
-                     "note": "one persistent workgroup per chain: latency-bound by design (see DESIGN.md)"},
+        "roofline": chain_roofline("k_chain_run", model_bytes(P, int(ctx.n), N), a.iters_per_step * C, avg_s,
+                                   bytes_per_launch, "k_chain_run/single",
+                                   C == 1 and ladder is None and N == 5000 and a.iters_per_step == 5000),
     }
-    if C == 1 and ladder is None and N == 5000 and a.iters_per_step == 5000:
-        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = measured_traffic("k_chain_run/single")
     if ladder is not None:
         out["tempering"] = {"replicas": ladder.R, "temps": [round(t, 4) for t in ladder.temps],
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
@@ -279,16 +314,13 @@ def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3):
     for c in chains:
         c.close()
     value = C * iters * steps / el
-    tr, src = measured_traffic("k_chain_run/many256")
-    achieved = nbytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+    avg_s = kms / 1e3 / max(launches, 1)
+    roof = chain_roofline("k_chain_run (grid = %d chains)" % C, model_bytes(int(ctx.P), int(ctx.n), len(model.xCell)),
+                          C * iters, avg_s, nbytes / max(launches, 1), "k_chain_run/many256", C == 256 and iters == 1000)
+    roof["note"] = ("the full-evaluate byte model exceeds HBM peak here: the incremental kernel does not read what a "
+                    "full evaluate reads (its working set stays in LDS / L2), see frac_measured_traffic")
     return {"chains": C, "proposals_per_s": round(value, 1), "per_chain_proposals_per_s": round(value / C, 1),
-            "ms_per_launch": round(kms / max(launches, 1), 4), "iters_per_launch": iters,
-            "roofline": {"kernel": "k_chain_run (grid = %d chains)" % C, "bound": "hbm",
-                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "algorithmic_bytes_per_launch": round(nbytes / max(launches, 1), 1),
-                         "traffic": tr if C == 256 and iters == 1000 else None,
-                         "traffic_source": src if C == 256 and iters == 1000 else None}}
+            "ms_per_launch": round(kms / max(launches, 1), 4), "iters_per_launch": iters, "roofline": roof}
 
 
 def full_evaluate(tt, ctx, model, N, reps=50):
@@ -341,11 +373,18 @@ def stress(tt, chain_iters=2000):
     prm = tt.define_TDstructrure().replace(max_cells=40000)
     ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=77, chain=1), model)
     ch.run(200)
+    b0 = ch.stats()["bytes"]
+    ctx.timing(enable=True, reset=True)
     t0 = time.perf_counter()
     ch.run(chain_iters)
     el = time.perf_counter() - t0
+    launches, kms = ctx.timing(kernel="chain_run")
+    ctx.timing(enable=False)
     res["chain"] = {"proposals_per_s": round(chain_iters / el, 1), "iters": chain_iters,
-                    "layout": "hbm (tiles, rays, order do not fit in LDS)"}
+                    "layout": "hbm (tiles, rays, order do not fit in LDS)",
+                    "roofline": chain_roofline("k_chain_run<false>", model_bytes(int(ctx.P), int(ctx.n), 20000),
+                                               chain_iters, kms / 1e3 / max(launches, 1), ch.stats()["bytes"] - b0,
+                                               "k_chain_run/stress", chain_iters == 2000)}
     ch.close()
     ctx.close()
     return res

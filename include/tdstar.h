@@ -97,6 +97,13 @@ int td_set_sigma(td_ctx *ctx, const double *allSig);
  *          (what v_nearest computes but never returns)  (nullable)
  * phi is the sequential chi^2 of MCsub.jl:170-172 and ptS uses Julia's sum
  * association (oracle/README.md), so both are bit-exact to the CPU oracle.
+ * Incremental path: when the cells are the previous call's model (or the model
+ * before it) plus ONE reference-shaped edit -- an appended cell (birth,
+ * TD_inversion_function.jl:85-88), a deleted one (death, :132-135), one new
+ * zeta (change, :189) or one new site (move, :234-236) -- and nearest_out is
+ * NULL, the context evaluates only what the edit changes on a device-resident
+ * copy of the chain state (the DEVICE engine's algorithm); the results are
+ * bit-identical to the full evaluate.  Other calls evaluate in full.
  * ------------------------------------------------------------------------ */
 int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const double *zCell,
                 const double *zeta, int64_t nCells, int debug_prior, double *ptS_out, double *phi_out,
@@ -187,6 +194,11 @@ typedef struct td_chain_params {
  * the parity reference for the DEVICE engine. */
 #define TD_ENGINE_DEVICE 0
 #define TD_ENGINE_HOST 1
+/* DROPIN: the host loop of HOST, calling the PUBLIC td_evaluate /
+ * td_interpolate exactly as the unchanged Julia host would (td_evaluate's
+ * incremental path then follows the chain on the device).  Measures the
+ * drop-in boundary; same trajectory as the other two. */
+#define TD_ENGINE_DROPIN 2
 
 typedef struct td_chain_stats {
     int64_t iterations;        /* proposals drawn so far */

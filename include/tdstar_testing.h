@@ -88,6 +88,10 @@ int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, dou
  * the reference's own model.jld phi values.  1 <= n <= 4096.  Needs a GPU. */
 int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]);
 
+/* td_evaluate's incremental path on (1, default) or off (0: every call is a
+ * full evaluate; the shadow chain is released). */
+int tdt_set_incremental(td_ctx *ctx, int on);
+
 /* Nearest-cell method of td_evaluate / td_interpolate: 0 auto (bucket grid
  * from 256 cells on), 1 brute force (every point x every cell), 2 bucket grid.
  * All give the same answer (the lexicographic (distance, index) minimum). */

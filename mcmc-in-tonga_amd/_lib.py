@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libtdstar.so")
 
 TD_OK, TD_ERR_ARG, TD_ERR_LAYOUT, TD_ERR_HIP, TD_ERR_NOMEM, TD_ERR_BOUNDS = range(6)
-TD_ENGINE_DEVICE, TD_ENGINE_HOST = 0, 1
+TD_ENGINE_DEVICE, TD_ENGINE_HOST, TD_ENGINE_DROPIN = 0, 1, 2
 
 _d = ctypes.c_double
 _i32 = ctypes.c_int32
@@ -86,6 +86,7 @@ SIGNATURES = {
     "tdt_block_delta_sum": (ctypes.c_int, [ctypes.c_int, _pd, _pd, _pd, _pi32, _i64, _i64, _pd, _pd,
                                             ctypes.POINTER(ctypes.c_int64), _pi32]),
     "tdt_wave_seq_sum": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _d, _pd, _pd, _pi32]),
+    "tdt_set_incremental": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_chi2": (ctypes.c_int, [_vp, _pd, ctypes.c_int, _pd]),
     "tdt_accept": (ctypes.c_int, [ctypes.POINTER(TdChainParams), ctypes.c_int, _d, _d, _i64, _d, _d, _d, _d, _d]),
 }

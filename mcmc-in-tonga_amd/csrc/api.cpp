@@ -188,6 +188,27 @@ hipError_t nearest_uploaded(td_ctx *ctx, const double *qx, const double *qy, con
                           ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm);
 }
 
+int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                  int64_t ncells, double *ptS_out, double *phi_out, int32_t *nearest_out) {
+    int rc = upload_cells(ctx, x, y, z, zeta, ncells);
+    if (rc) return rc;
+    const auto &g = ctx->g;
+    Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
+    hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, ncells, ctx->best_i, ctx->best_d, ctx->zeta0);
+    if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
+    // [phi, ptS] land in pinned host memory straight from the kernel (no copy back)
+    e = launch_ray_sums_chi2(g, ctx->zeta0, ctx->ptS, ctx->phi, ctx->stream, tm, ctx->h_out_dev);
+    if (e != hipSuccess) return hip_err(ctx, e, "ray-sum / chi2 kernel");
+    if (nearest_out && g.P)
+        TD_HIP(ctx, hipMemcpyAsync(ctx->h_best_i, ctx->best_i, sizeof(int) * (size_t)g.P, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    TD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (phi_out) *phi_out = ctx->h_out[0];
+    if (ptS_out && g.n) std::memcpy(ptS_out, ctx->h_out + 1, sizeof(double) * (size_t)g.n);
+    if (nearest_out && g.P) std::memcpy(nearest_out, ctx->h_best_i, sizeof(int) * (size_t)g.P);
+    return TD_OK;
+}
+
 }  // namespace tdstar
 
 using namespace tdstar;
@@ -197,6 +218,7 @@ namespace {
 void free_ctx(td_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    shadow_free(c);
     c->timer.release();
     void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->g.done, c->cells,
                    c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->phi,
@@ -366,6 +388,7 @@ int td_get_info(const td_ctx *ctx, td_info *info) {
 int td_set_sigma(td_ctx *ctx, const double *allSig) {
     if (!ctx || (!allSig && ctx->g.n > 0)) return set_err(ctx, TD_ERR_ARG, "td_set_sigma: NULL");
     TD_HIP(ctx, hipSetDevice(ctx->device));
+    shadow_free(ctx);  // the shadow chain's chi^2 terms were for the old sigma
     ctx->sig_host.assign(allSig, allSig + ctx->g.n);
     ctx->likelihood = likelihood_constant(allSig, ctx->g.n);
     if (ctx->g.n)
@@ -386,22 +409,10 @@ int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const dou
         return set_err(ctx, TD_ERR_ARG, "td_evaluate: bad cell arrays");
     if (nCells > 0x7fffffff) return set_err(ctx, TD_ERR_ARG, "td_evaluate: too many cells");
     TD_HIP(ctx, hipSetDevice(ctx->device));
-    int rc = upload_cells(ctx, xCell, yCell, zCell, zeta, nCells);
+    int rc = (nearest_out || !ctx->incremental)
+                 ? evaluate_full(ctx, xCell, yCell, zCell, zeta, nCells, ptS_out, phi_out, nearest_out)
+                 : evaluate_incremental(ctx, xCell, yCell, zCell, zeta, nCells, ptS_out, phi_out);
     if (rc) return rc;
-    const auto &g = ctx->g;
-    Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
-    hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, nCells, ctx->best_i, ctx->best_d, ctx->zeta0);
-    if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
-    // [phi, ptS] land in pinned host memory straight from the kernel (no copy back)
-    e = launch_ray_sums_chi2(g, ctx->zeta0, ctx->ptS, ctx->phi, ctx->stream, tm, ctx->h_out_dev);
-    if (e != hipSuccess) return hip_err(ctx, e, "ray-sum / chi2 kernel");
-    if (nearest_out && g.P)
-        TD_HIP(ctx, hipMemcpyAsync(ctx->h_best_i, ctx->best_i, sizeof(int) * (size_t)g.P, hipMemcpyDeviceToHost,
-                                   ctx->stream));
-    TD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (phi_out) *phi_out = ctx->h_out[0];
-    if (ptS_out && g.n) std::memcpy(ptS_out, ctx->h_out + 1, sizeof(double) * (size_t)g.n);
-    if (nearest_out && g.P) std::memcpy(nearest_out, ctx->h_best_i, sizeof(int) * (size_t)g.P);
     if (likelihood_out) *likelihood_out = ctx->likelihood;  // MCsub.jl:179-182: model-independent
     return TD_OK;
 }
@@ -414,11 +425,14 @@ int td_evaluate_batch(td_ctx *ctx, int64_t nmodels, const int64_t *cell_off, con
     for (int64_t k = 0; k < nmodels; ++k) {
         const int64_t a = cell_off[k], b = cell_off[k + 1];
         if (b < a || a < 0) return set_err(ctx, TD_ERR_ARG, "td_evaluate_batch: offsets not monotone");
-        int rc = td_evaluate(ctx, xCell ? xCell + a : nullptr, yCell ? yCell + a : nullptr,
-                             zCell ? zCell + a : nullptr, zeta ? zeta + a : nullptr, b - a, 0,
-                             ptS_out ? ptS_out + k * ctx->g.n : nullptr, phi_out ? phi_out + k : nullptr,
-                             likelihood_out ? likelihood_out + k : nullptr, nullptr);
+        if (b > a && (!xCell || !yCell || !zCell || !zeta))
+            return set_err(ctx, TD_ERR_ARG, "td_evaluate_batch: bad cell arrays");
+        TD_HIP(ctx, hipSetDevice(ctx->device));
+        // independent models: the full evaluate (no shadow chain)
+        int rc = evaluate_full(ctx, xCell + a, yCell + a, zCell + a, zeta + a, b - a,
+                               ptS_out ? ptS_out + k * ctx->g.n : nullptr, phi_out ? phi_out + k : nullptr);
         if (rc) return rc;
+        if (likelihood_out) likelihood_out[k] = ctx->likelihood;
     }
     return TD_OK;
 }
@@ -589,6 +603,13 @@ int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]) {
     if (scratch) (void)hipFree(scratch);
     if (dout) (void)hipFree(dout);
     if (e != hipSuccess) return hip_err(ctx, e, "tdt_chi2");
+    return TD_OK;
+}
+
+int tdt_set_incremental(td_ctx *ctx, int on) {
+    if (!ctx || on < 0 || on > 1) return TD_ERR_ARG;
+    ctx->incremental = on;
+    if (!on) shadow_free(ctx);
     return TD_OK;
 }
 

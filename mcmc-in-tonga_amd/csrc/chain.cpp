@@ -41,6 +41,7 @@ struct td_chain {
     ChainScalars *st_dev = nullptr;
     ChainScalars *st_host = nullptr;  // pinned
     NNWork nn;
+    double *script_host = nullptr;  // pinned, mapped: [phi_n, ptS_n] of a scripted step (shadow chains)
 };
 
 namespace {
@@ -107,10 +108,16 @@ void build_starting(td_chain *ch) {
     }
 }
 
+// HOST: the full evaluate of every proposed model (the parity reference);
+// DROPIN: the public td_evaluate, i.e. what an unchanged Julia host calls
+// (its incremental path follows the chain on the device, incremental.cpp)
 int host_evaluate(td_chain *ch, const std::vector<double> &x, const std::vector<double> &y,
                   const std::vector<double> &z, const std::vector<double> &zeta, double *phi, double *ptS) {
-    return td_evaluate(ch->ctx, x.data(), y.data(), z.data(), zeta.data(), (int64_t)x.size(),
-                       ch->prm.debug_prior, ptS, phi, nullptr, nullptr);
+    if (ch->engine == TD_ENGINE_DROPIN || ch->prm.debug_prior == 1)
+        return td_evaluate(ch->ctx, x.data(), y.data(), z.data(), zeta.data(), (int64_t)x.size(),
+                           ch->prm.debug_prior, ptS, phi, nullptr, nullptr);
+    TD_HIP(ch->ctx, hipSetDevice(ch->ctx->device));
+    return evaluate_full(ch->ctx, x.data(), y.data(), z.data(), zeta.data(), (int64_t)x.size(), ptS, phi);
 }
 
 int host_interp1(td_chain *ch, const std::vector<double> &x, const std::vector<double> &y,
@@ -438,6 +445,7 @@ void free_chain(td_chain *ch) {
     if (ch->ctx && ch->ctx->stream) (void)hipStreamSynchronize(ch->ctx->stream);
     if (ch->dev_block) (void)hipFree(ch->dev_block);
     if (ch->st_host) (void)hipHostFree(ch->st_host);
+    if (ch->script_host) (void)hipHostFree(ch->script_host);
     if (ch->nn.part_d) (void)hipFree(ch->nn.part_d);
     if (ch->nn.part_i) (void)hipFree(ch->nn.part_i);
     delete ch;
@@ -458,7 +466,7 @@ int td_chain_create(td_chain **out, td_ctx *ctx, const td_chain_params *params, 
         return set_err(ctx, TD_ERR_ARG, "td_chain_create: bad cell bounds / sig / zeta_scale");
     if (!(p.xmax >= p.xmin && p.ymax >= p.ymin && p.zmax >= p.zmin))
         return set_err(ctx, TD_ERR_ARG, "td_chain_create: empty box");
-    if (p.engine != TD_ENGINE_DEVICE && p.engine != TD_ENGINE_HOST)
+    if (p.engine != TD_ENGINE_DEVICE && p.engine != TD_ENGINE_HOST && p.engine != TD_ENGINE_DROPIN)
         return set_err(ctx, TD_ERR_ARG, "td_chain_create: unknown engine");
     if (nCells < 0 || (nCells > 0 && (!xCell || !yCell || !zCell || !zeta)))
         return set_err(ctx, TD_ERR_ARG, "td_chain_create: bad cell arrays");
@@ -485,7 +493,7 @@ int td_chain_create(td_chain **out, td_ctx *ctx, const td_chain_params *params, 
         return rc;
     }
     int rc = TD_OK;
-    if (ch->engine == TD_ENGINE_HOST) {
+    if (ch->engine != TD_ENGINE_DEVICE) {
         rc = host_evaluate(ch, ch->x, ch->y, ch->z, ch->zeta, &ch->phi, ch->ptS.data());  // build_starting :118
         if (!rc) ch->stats.evaluations = 1;
     } else {
@@ -513,7 +521,7 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
     if (iterations == 0) return TD_OK;
     hipError_t e = hipSetDevice(ch->ctx->device);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "hipSetDevice");
-    if (ch->engine == TD_ENGINE_HOST) {
+    if (ch->engine != TD_ENGINE_DEVICE) {
         for (int64_t i = 0; i < iterations; ++i) {
             int rc = host_iteration(ch);
             if (rc) return rc;
@@ -544,7 +552,7 @@ int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterati
     for (int64_t b = 0; b < nchains; ++b) {
         if (!chains[b] || chains[b]->ctx != c)
             return set_err(c, TD_ERR_ARG, "td_chain_run_batch: every chain must be non-NULL and share one context");
-        host |= chains[b]->engine == TD_ENGINE_HOST;
+        host |= chains[b]->engine != TD_ENGINE_DEVICE;
         for (int64_t k = 0; k < b; ++k)
             if (chains[k] == chains[b]) return set_err(c, TD_ERR_ARG, "td_chain_run_batch: a chain appears twice");
     }
@@ -637,6 +645,74 @@ int td_chain_set_temperature(td_chain *ch, double temperature) {
     ch->dev.params = ch->P;
     return TD_OK;
 }
+
+}  // extern "C"
+
+// ------------------------------------------------ td_evaluate's shadow ----
+namespace tdstar {
+
+int shadow_chain_create(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                        int64_t ncells, int64_t cap, const double box[6], td_chain **out) {
+    *out = nullptr;
+    td_chain_params p{};
+    p.debug_prior = 0;
+    p.sig = 10;
+    p.zeta_scale = 50;
+    p.max_cells = (int32_t)std::max<int64_t>(cap - 1, ncells);
+    p.min_cells = 1;
+    p.prior = 1;
+    p.n_iter = p.burn_in = p.keep_each = 1.0;
+    p.xmin = box[0]; p.xmax = box[1]; p.ymin = box[2]; p.ymax = box[3]; p.zmin = box[4]; p.zmax = box[5];
+    p.temperature = 1.0;
+    p.engine = TD_ENGINE_DEVICE;
+    td_chain *ch = nullptr;
+    int rc = td_chain_create(&ch, ctx, &p, x, y, z, zeta, ncells);
+    if (rc) return rc;
+    hipError_t e = hipHostMalloc(&ch->script_host, sizeof(double) * ((size_t)ctx->g.n + 1),
+                                 hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&ch->dev.script_out), ch->script_host, 0);
+    if (e != hipSuccess) {
+        free_chain(ch);
+        return hip_err(ctx, e, "hipHostMalloc(shadow output)");
+    }
+    *out = ch;
+    return TD_OK;
+}
+
+int64_t shadow_chain_slots(const td_chain *ch) { return ch->dev.cap; }
+int64_t shadow_chain_ncells(const td_chain *ch) { return ch->stats.ncells; }
+double shadow_chain_phi(const td_chain *ch) { return ch->phi; }
+
+// Run 1..kMaxScript host-given steps in one k_chain_run launch; the step with
+// decision 0 (the last) leaves [phi_n, ptS_n] in the pinned output.
+int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, double *phi_out, double *ptS_out) {
+    td_ctx *c = ch->ctx;
+    if (nsteps < 1 || nsteps > kMaxScript) return set_err(c, TD_ERR_ARG, "shadow script");
+    ch->dev.nscript = nsteps;
+    for (int k = 0; k < nsteps; ++k) ch->dev.script[k] = steps[k];
+    Timer *tm = c->timer.on ? &c->timer : nullptr;
+    hipEvent_t t0 = tm ? tm->begin(c->stream) : nullptr;
+    hipError_t e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, c->stream);
+    ch->dev.nscript = 0;
+    if (e != hipSuccess) return hip_err(c, e, "shadow descriptor upload");
+    e = chain_run(&ch->dev, ch->dev_ptr, 1, nsteps, c->stream);
+    if (tm) tm->end("chain_script", t0, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (script)");
+    e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "k_chain_run (script)");
+    adopt_scalars(ch);
+    if (steps[nsteps - 1].decision == 0) {
+        if (phi_out) *phi_out = ch->script_host[0];
+        if (ptS_out && c->g.n) std::memcpy(ptS_out, ch->script_host + 1, sizeof(double) * (size_t)c->g.n);
+    }
+    return TD_OK;
+}
+
+void shadow_chain_destroy(td_chain *ch) { free_chain(ch); }
+
+}  // namespace tdstar
+
+extern "C" {
 
 // --------------------------------------------------------- testing hooks ----
 void tdt_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {

@@ -22,6 +22,7 @@
 
 #include "chain_logic.h"
 #include "internal.h"
+#include "../../include/tdstar.h"
 
 namespace tdstar {
 
@@ -50,6 +51,21 @@ struct ChainScalars {
     int last_accept;       // 123,179,217,249): the proposal drawn and whether it was accepted
     int pad;
 };
+
+// A proposal given by the host instead of drawn (td_evaluate's incremental
+// path: the caller's new model is the chain's model with one edit, as the
+// reference's proposals are -- TD_inversion_function.jl:85-88 append!, :132-135
+// deleteat!, :189 zeta, :234-236 site).  decision: 1 = commit it (the caller
+// went on from it), 0 = evaluate it, report phi and ptS, and undo it.
+struct ScriptStep {
+    int action;      // 1 birth, 2 death, 3 change, 4 move
+    int index;       // Julia position (0-based) of the killed / changed / moved cell
+    double x, y, z;  // birth site / move target
+    double zeta;     // birth / change value
+    int decision;
+    int pad;
+};
+constexpr int kMaxScript = 2;
 
 struct DevChain {
     // geometry (owned by the td_ctx)
@@ -95,6 +111,12 @@ struct DevChain {
     int *bucket_count;      // [G]
     BucketEntry *buckets;   // [G * kBucketCap]
     int *grid_overflow;     // sticky: a bucket overflowed -> always scan all cells
+    // scripted launches (nscript > 0: iteration k runs script[k] instead of a draw;
+    // no early rejection, the decision is the step's): a step with decision 0 writes
+    // [phi_n, ptS_n[0..n)] to script_out (pinned host memory, device address)
+    int nscript;
+    ScriptStep script[kMaxScript];
+    double *script_out;
 };
 
 // Build the cache from scratch for the cells currently in slots 0..ncells-1
@@ -112,6 +134,15 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
 // the restart from n/2 (path 3 only).  scratch: 3n + 16 doubles.
 hipError_t test_chain_chi2(const double *ptS, const double *tS, const double *sig, int n, int path, double *scratch,
                            double *out, hipStream_t s);
+// td_evaluate's incremental path (incremental.cpp): a device chain that never
+// draws -- it takes the caller's edits as scripted steps (ScriptStep).
+int shadow_chain_create(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                        int64_t ncells, int64_t cap, const double box[6], td_chain **out);
+int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, double *phi_out, double *ptS_out);
+int64_t shadow_chain_slots(const td_chain *ch);
+int64_t shadow_chain_ncells(const td_chain *ch);
+double shadow_chain_phi(const td_chain *ch);
+void shadow_chain_destroy(td_chain *ch);
 // LDS bytes of the two layouts, whether super-tiles fit, and the layout chain_run takes.
 void chain_lds_sizes(const DevChain &d, int64_t out[4]);
 

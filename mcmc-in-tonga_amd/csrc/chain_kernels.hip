@@ -116,6 +116,44 @@ __device__ __forceinline__ void make_proposal(PState &o, const tdchain::Params &
     o.eval = q.active && (q.valid || q.action == tdchain::kBirth) && P.debug_prior != 1;
 }
 
+// A scripted step (td_evaluate's incremental path) as the proposal: always
+// active and valid, no draws; birth's zeta is given (birth_zeta is not called).
+template <class SlotAt>
+__device__ __forceinline__ void script_proposal(PState &o, const ScriptStep &st, int nfree, int nslots,
+                                               const int *free_slots, const double *cx, const double *cy,
+                                               const double *cz, const double *czeta, SlotAt slot_at) {
+    Proposal q{};
+    q.action = st.action;
+    q.active = 1;
+    q.valid = 1;
+    q.index = st.index;
+    q.x = st.x;
+    q.y = st.y;
+    q.z = st.z;
+    q.zeta = st.zeta;
+    o.slot_k = -1;
+    o.new_slot = -1;
+    if (q.action != tdchain::kBirth) {
+        const int s = slot_at(st.index);
+        o.slot_k = s;
+        o.kx = cx[s];
+        o.ky = cy[s];
+        o.kz = cz[s];
+        o.zeta_killed = czeta[s];
+        if (q.action == tdchain::kChange) {  // the site stays; only zeta is new
+            q.x = o.kx;
+            q.y = o.ky;
+            q.z = o.kz;
+        } else if (q.action == tdchain::kMove) {
+            q.zeta = o.zeta_killed;
+        }
+    } else {
+        o.new_slot = nfree > 0 ? free_slots[nfree - 1] : nslots;
+    }
+    o.p = q;
+    o.eval = 1;
+}
+
 struct Shared {
     PState ps[2];      // this iteration's proposal (ps[cur]) and the next one guessed in phase F
     int cur, spec_ok;
@@ -516,6 +554,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const tdchain::Params &P = d.params;
     const int n = d.n, NT = d.ntiles;
     const bool prof_on = d.profile != 0;
+    const int nscript = d.nscript;  // > 0: host-given proposals (td_evaluate), iters == nscript
 
     // ---- views: LDS copies of the tile / ray / order arrays when they fit ----
     Views v;
@@ -631,11 +670,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     // the draws (and their normal quantiles) of 64 iterations, one lane each:
     // a function of (seed, chain, iteration) only; and the first proposal
     if (wv == 0) {
-        draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
+        if (!nscript) draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
         wave_sync_lds();
         if (lane == 0 && iters > 0) {
-            make_proposal(sh.ps[0], P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
-                          d.czeta, [&](int pos) { return v.ord[pos]; });
+            if (nscript)
+                script_proposal(sh.ps[0], d.script[0], sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz, d.czeta,
+                                [&](int pos) { return v.ord[pos]; });
+            else
+                make_proposal(sh.ps[0], P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
+                              d.czeta, [&](int pos) { return v.ord[pos]; });
             if (sh.ps[0].p.active) sh.proposed[sh.ps[0].p.action] += 1;
             sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
             sh.pts_seen = sh.ray_pts = 0;
@@ -690,7 +733,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         STAMP(0);
         if (p.active) {
             // ============ phase B: tile pass || birth/death Interpolation ============
-            const bool query = action == tdchain::kBirth || action == tdchain::kDeath;
+            // (a scripted step brings its own values: no Interpolation query)
+            const bool query = !nscript && (action == tdchain::kBirth || action == tdchain::kDeath);
             if (eval) {
                 // tiles whose box can hold a point the proposal changes (the last
                 // wave answers the Interpolation query meanwhile)
@@ -782,10 +826,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             if (action == tdchain::kDeath) zetanew_death = sh.q_zeta;
         }
         Proposal pp = p;
-        if (p.active && action == tdchain::kBirth) tdchain::birth_zeta(P, pp, czeta);  // every lane, same value
+        if (p.active && action == tdchain::kBirth && !nscript) tdchain::birth_zeta(P, pp, czeta);  // every lane, same value
         STAMP(1);
         // the next iteration's proposal can be guessed during phase F if its draws are here
-        const bool can_spec = it + 1 < iters && ((it + 1) & 63) != 0;
+        const bool can_spec = !nscript && it + 1 < iters && ((it + 1) & 63) != 0;
         if (pp.active && pp.valid) {
             const bool fwd = P.debug_prior != 1;
             int no = 0;
@@ -938,8 +982,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // Metropolis-Hastings decision (a proven rejection skips the rest of the sum:
                 // accept() on the exact phi_n would reject too)
                 const bool early = fwd && k0 < n && sh.early_reject;
-                const bool acc = !early && tdchain::accept(P, pp, phi_r, phi_n, czeta, zeta_killed,
-                                                           zetanew_death, sh.lnN);
+                const bool acc = nscript ? d.script[it].decision != 0
+                                         : !early && tdchain::accept(P, pp, phi_r, phi_n, czeta, zeta_killed,
+                                                                     zetanew_death, sh.lnN);
                 acc_r = acc;
                 sh.accept = acc ? 1 : 0;
                 sh.phi_n = phi_n;
@@ -996,7 +1041,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // non-negative terms is within n ulps of any other association; above
                 // the rejection bound by a wide margin, the proposal is rejected
                 const int k0 = sh.k0;
-                if (!WALK && fwd && k0 < n) {
+                if (!WALK && fwd && k0 < n && !nscript) {
                     double part = 0.0;
                     for (int k = k0 + lane; k < n; k += 64) part = part + v.term[k];
                     const double S = wave_sum_f64(part);
@@ -1030,6 +1075,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             STAMP(5);
             // ================= phase G: commit (or undo) =================
             const int nc = sh.n_changed, nr = sh.n_rays;
+            if (nscript && d.script[it].decision == 0) {  // report phi_n and the proposed model's ptS
+                double *out = d.script_out;
+                for (int r = tid; r < n; r += kChainThreads) out[1 + r] = v.rflag[r] ? v.cptS[r] : v.ptS[r];
+                if (tid == 0) out[0] = sh.phi_n;
+            }
             if (sh.accept) {
                 const int nt = sh.n_tiles, k0 = sh.k0;
                 for (int c = tid; c < nc; c += kChainThreads) {
@@ -1115,7 +1165,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         if (wv == 0) {
             if (prof_on && lane == 0) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
             if (it + 1 < iters) {
-                if (((it + 1) & 63) == 0) {
+                if (((it + 1) & 63) == 0 && !nscript) {
                     wave_sync_lds();
                     draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(iter0 + it + 1 + lane));
                     wave_sync_lds();
@@ -1133,10 +1183,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     } else {
                         // a just-killed position: later positions read the pre-shift order
                         const int killed = (acc && action == tdchain::kDeath) ? (int)pp.index : -1;
-                        make_proposal(sh.ps[cur_r], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots, d.free_slots,
-                                      d.cx, d.cy, d.cz, d.czeta, [&](int pos) {
-                                          return (killed >= 0 && pos >= killed) ? d.order_tmp[pos + 1] : v.ord[pos];
-                                      });
+                        auto slot_at = [&](int pos) {
+                            return (killed >= 0 && pos >= killed) ? d.order_tmp[pos + 1] : v.ord[pos];
+                        };
+                        if (nscript)
+                            script_proposal(sh.ps[cur_r], d.script[it + 1], sh.nfree, sh.nslots, d.free_slots, d.cx,
+                                            d.cy, d.cz, d.czeta, slot_at);
+                        else
+                            make_proposal(sh.ps[cur_r], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots,
+                                          d.free_slots, d.cx, d.cy, d.cz, d.czeta, slot_at);
                     }
                     const tdchain::Proposal &np = sh.ps[cur_r].p;
                     if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);

@@ -9,6 +9,10 @@
 #include "../../include/tdstar.h"
 #include "internal.h"
 
+namespace tdstar {
+struct td_shadow;
+}
+
 struct td_ctx {
     int device = 0;
     int num_cus = 0;
@@ -57,6 +61,8 @@ struct td_ctx {
     void *chain_desc = nullptr;         // device array of chain descriptors (td_chain_run_batch)
     size_t chain_desc_bytes = 0;
     void *h_chain_desc = nullptr;       // pinned staging of the same
+    tdstar::td_shadow *shadow = nullptr;  // td_evaluate's incremental path (incremental.cpp)
+    int incremental = 1;                // 0: td_evaluate always evaluates in full (tdt_set_incremental)
     std::string err;
 };
 
@@ -87,5 +93,13 @@ hipError_t nearest_uploaded(td_ctx *ctx, const double *qx, const double *qy, con
 // Julia Base.sum association (see oracle/README.md); used for the likelihood constant.
 double julia_sum(const double *a, int64_t n);
 double likelihood_constant(const double *sig, int64_t n);
+// td_evaluate's full path: nearest search over every point, ray sums, chi^2
+// (nearest_out nullable).  The HOST chain engine calls it directly.
+int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                  int64_t ncells, double *ptS_out, double *phi_out, int32_t *nearest_out = nullptr);
+// td_evaluate's incremental path (incremental.cpp): phi and ptS only.
+int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                         int64_t ncells, double *ptS_out, double *phi_out);
+void shadow_free(td_ctx *ctx);
 
 }  // namespace tdstar

@@ -1,0 +1,276 @@
+// incremental.cpp -- td_evaluate's incremental path: the drop-in boundary
+// running the device chain's algorithm for an UNCHANGED Julia host.
+//
+// The reference's chain (TD_inversion_function.jl:70-274) calls evaluate on
+// modeln = deepcopy(model) plus ONE edit: append! (birth, :85-88),
+// deleteat! (death, :132-135), a new zeta (change, :189) or a new site (move,
+// :234-236); if it accepts, the next modeln is an edit of this one, else of
+// the previous model.  So every call's cells are one edit away from either the
+// last committed model B or the last evaluated proposal Q = B + e.  The
+// context keeps a "shadow" device chain holding B (per-point nearest cell,
+// tiles, ray sums, chi^2 prefix sums -- chain_dev.h) and evaluates each
+// recognised edit incrementally in one k_chain_run launch (scripted steps,
+// no draws): when the new cells are an edit of Q, e is committed first (Julia
+// accepted it), then the new edit is evaluated and undone.  The result is
+// bit-identical to the full evaluate (the same invariant as the device chain,
+// tests/test_gpu_incremental.py).  Anything else -- the first call, unrelated
+// models, several edits at once, cells outside a sane range, nearest indices
+// requested -- takes the full evaluate, and a shadow is built from a model
+// only once the next call turns out to be an edit of it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "chain_dev.h"
+#include "ctx.h"
+
+namespace tdstar {
+
+struct Cells {
+    std::vector<double> x, y, z, zeta;
+    int64_t size() const { return (int64_t)x.size(); }
+    void assign(const double *a, const double *b, const double *c, const double *d, int64_t n) {
+        x.assign(a, a + n);
+        y.assign(b, b + n);
+        z.assign(c, c + n);
+        zeta.assign(d, d + n);
+    }
+    void apply(const ScriptStep &e) {
+        const size_t k = (size_t)e.index;
+        switch (e.action) {
+            case 1: x.push_back(e.x); y.push_back(e.y); z.push_back(e.z); zeta.push_back(e.zeta); break;
+            case 2:
+                x.erase(x.begin() + (long)k); y.erase(y.begin() + (long)k);
+                z.erase(z.begin() + (long)k); zeta.erase(zeta.begin() + (long)k);
+                break;
+            case 3: zeta[k] = e.zeta; break;
+            default: x[k] = e.x; y[k] = e.y; z[k] = e.z; break;
+        }
+    }
+};
+
+struct td_shadow {
+    td_chain *ch = nullptr;
+    Cells B;                 // committed model (Julia order), what the shadow chain holds
+    double phiB = 0.0;
+    std::vector<double> ptSB;
+    bool pending = false;    // Q = B + e evaluated (and undone on the device)
+    ScriptStep e{};
+    double phiQ = 0.0;
+    std::vector<double> ptSQ;
+    int64_t built_n = 0;     // cells when the shadow's bucket grid was sized
+    // the last fully evaluated model, a shadow candidate
+    bool have_last = false;
+    Cells last;
+    double last_phi = 0.0;
+    std::vector<double> last_ptS;
+};
+
+namespace {
+
+constexpr double kSane = 1e6;  // |coordinate| bound for the shadow (distances stay far below the 1e9 sentinel)
+
+bool sane(double v) { return std::isfinite(v) && std::fabs(v) <= kSane; }
+
+bool bits_eq(const double *a, const double *b, int64_t n) {
+    return n <= 0 || std::memcmp(a, b, sizeof(double) * (size_t)n) == 0;
+}
+
+// first position where (x, y, z, zeta) differ bit-wise, up to n
+int64_t common_prefix(const double *const in[4], const Cells &b, int64_t n) {
+    const double *base[4] = {b.x.data(), b.y.data(), b.z.data(), b.zeta.data()};
+    int64_t lim = n;
+    for (int a = 0; a < 4; ++a) {
+        int64_t k = 0;
+        constexpr int64_t kBlk = 64;
+        while (k + kBlk <= lim && bits_eq(in[a] + k, base[a] + k, kBlk)) k += kBlk;
+        while (k < lim && std::memcmp(in[a] + k, base[a] + k, sizeof(double)) == 0) ++k;
+        lim = k;
+    }
+    return lim;
+}
+
+// Is `in` (M cells) `base` plus one reference-shaped edit?  0: identical,
+// 1: one edit (in *e, decision unset), -1: neither.
+int classify(const double *const in[4], int64_t M, const Cells &base, ScriptStep *e) {
+    const int64_t N = base.size();
+    const int64_t p = common_prefix(in, base, std::min(M, N));
+    std::memset(e, 0, sizeof *e);
+    if (M == N) {
+        if (p == N) return 0;
+        const int64_t t = N - p - 1;  // the rest must be unchanged
+        if (!bits_eq(in[0] + p + 1, base.x.data() + p + 1, t) || !bits_eq(in[1] + p + 1, base.y.data() + p + 1, t) ||
+            !bits_eq(in[2] + p + 1, base.z.data() + p + 1, t) || !bits_eq(in[3] + p + 1, base.zeta.data() + p + 1, t))
+            return -1;
+        const bool site = bits_eq(in[0] + p, base.x.data() + p, 1) && bits_eq(in[1] + p, base.y.data() + p, 1) &&
+                          bits_eq(in[2] + p, base.z.data() + p, 1);
+        const bool val = bits_eq(in[3] + p, base.zeta.data() + p, 1);
+        e->index = (int)p;
+        if (site && !val) {  // change (:189)
+            if (!std::isfinite(in[3][p])) return -1;
+            e->action = 3;
+            e->zeta = in[3][p];
+            return 1;
+        }
+        if (!site && val) {  // move (:234-236)
+            if (!sane(in[0][p]) || !sane(in[1][p]) || !sane(in[2][p])) return -1;
+            e->action = 4;
+            e->x = in[0][p];
+            e->y = in[1][p];
+            e->z = in[2][p];
+            return 1;
+        }
+        return -1;
+    }
+    if (M == N + 1 && p == N) {  // birth: append! (:85-88)
+        if (!sane(in[0][N]) || !sane(in[1][N]) || !sane(in[2][N]) || !std::isfinite(in[3][N])) return -1;
+        e->action = 1;
+        e->index = (int)N;
+        e->x = in[0][N];
+        e->y = in[1][N];
+        e->z = in[2][N];
+        e->zeta = in[3][N];
+        return 1;
+    }
+    if (M == N - 1 && M >= 1) {  // death: deleteat!(kill) (:132-135)
+        const int64_t t = M - p;
+        if (!bits_eq(in[0] + p, base.x.data() + p + 1, t) || !bits_eq(in[1] + p, base.y.data() + p + 1, t) ||
+            !bits_eq(in[2] + p, base.z.data() + p + 1, t) || !bits_eq(in[3] + p, base.zeta.data() + p + 1, t))
+            return -1;
+        e->action = 2;
+        e->index = (int)p;
+        return 1;
+    }
+    return -1;
+}
+
+bool all_sane(const double *const in[4], int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+        if (!sane(in[0][i]) || !sane(in[1][i]) || !sane(in[2][i]) || !std::isfinite(in[3][i])) return false;
+    return true;
+}
+
+void drop_chain(td_shadow *s) {
+    if (s->ch) shadow_chain_destroy(s->ch);
+    s->ch = nullptr;
+    s->pending = false;
+}
+
+// Build the shadow chain from the last fully evaluated model.
+int build_shadow(td_ctx *ctx, td_shadow *s) {
+    drop_chain(s);
+    const Cells &c = s->last;
+    const int64_t n = c.size();
+    double box[6] = {HUGE_VAL, -HUGE_VAL, HUGE_VAL, -HUGE_VAL, HUGE_VAL, -HUGE_VAL};
+    const std::vector<double> *pts[3] = {&ctx->hx, &ctx->hy, &ctx->hz};
+    const std::vector<double> *cel[3] = {&c.x, &c.y, &c.z};
+    for (int a = 0; a < 3; ++a) {  // the cells' and the ray points' box: the bucket grid's extent
+        for (double v : *pts[a]) box[2 * a] = std::min(box[2 * a], v), box[2 * a + 1] = std::max(box[2 * a + 1], v);
+        for (double v : *cel[a]) box[2 * a] = std::min(box[2 * a], v), box[2 * a + 1] = std::max(box[2 * a + 1], v);
+        if (!(box[2 * a] <= box[2 * a + 1])) box[2 * a] = box[2 * a + 1] = 0.0;
+    }
+    const int64_t cap = std::max<int64_t>(2 * n, n + 256);
+    int rc = shadow_chain_create(ctx, c.x.data(), c.y.data(), c.z.data(), c.zeta.data(), n, cap, box, &s->ch);
+    if (rc) return rc;
+    s->B = c;
+    s->phiB = s->last_phi;
+    s->ptSB = s->last_ptS;
+    s->pending = false;
+    s->built_n = n;
+    return TD_OK;
+}
+
+}  // namespace
+
+void shadow_free(td_ctx *ctx) {
+    if (!ctx->shadow) return;
+    drop_chain(ctx->shadow);
+    delete ctx->shadow;
+    ctx->shadow = nullptr;
+}
+
+// td_evaluate without nearest indices (api.cpp); full = the plain evaluate.
+int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                         int64_t M, double *ptS_out, double *phi_out) {
+    if (!ctx->shadow) ctx->shadow = new td_shadow();
+    td_shadow *s = ctx->shadow;
+    const int64_t n = ctx->g.n;
+    const double *in[4] = {x, y, z, zeta};
+    auto out = [&](double phi, const std::vector<double> &ptS) -> int {
+        if (phi_out) *phi_out = phi;
+        if (ptS_out && n) std::memcpy(ptS_out, ptS.data(), sizeof(double) * (size_t)n);
+        return TD_OK;
+    };
+    auto full = [&]() -> int {  // the plain evaluate; its model becomes the shadow candidate
+        drop_chain(s);
+        s->have_last = false;
+        s->last_ptS.assign((size_t)n, 0.0);
+        int rc = evaluate_full(ctx, x, y, z, zeta, M, s->last_ptS.data(), &s->last_phi);
+        if (rc) return rc;
+        if (M >= 1 && n > 0 && all_sane(in, M)) {
+            s->last.assign(x, y, z, zeta, M);
+            s->have_last = true;
+        }
+        return out(s->last_phi, s->last_ptS);
+    };
+    if (!s->ch) {
+        ScriptStep e;
+        if (!s->have_last || classify(in, M, s->last, &e) < 0) return full();
+        int rc = build_shadow(ctx, s);  // the caller is walking a chain: follow it on the device
+        if (rc) return rc;
+    }
+    // which state is the new model an edit of?
+    ScriptStep e2;
+    ScriptStep steps[kMaxScript];
+    int nsteps = 0;
+    const int rb = classify(in, M, s->B, &e2);
+    if (rb == 0) return out(s->phiB, s->ptSB);
+    if (rb == 1 && s->pending && std::memcmp(&e2, &s->e, sizeof e2) == 0) return out(s->phiQ, s->ptSQ);  // == Q again
+    if (rb == 1) {
+        s->pending = false;  // Q (if any) was rejected: it is already undone
+    } else if (s->pending) {
+        Cells Q = s->B;
+        Q.apply(s->e);
+        const int rq = classify(in, M, Q, &e2);
+        if (rq < 0) return full();
+        if (rq == 0) return out(s->phiQ, s->ptSQ);
+        ScriptStep c = s->e;
+        c.decision = 1;  // Julia went on from Q: commit it first
+        steps[nsteps++] = c;
+        s->B.x.swap(Q.x), s->B.y.swap(Q.y), s->B.z.swap(Q.z), s->B.zeta.swap(Q.zeta);
+        s->phiB = s->phiQ;
+        s->ptSB.swap(s->ptSQ);
+        s->pending = false;
+    } else {
+        return full();
+    }
+    // slots: a birth needs a free one; regrow (rebuild) when the chain is full or the
+    // grid was sized for far fewer cells
+    const int64_t after = s->B.size() + (e2.action == 1 ? 1 : e2.action == 2 ? -1 : 0);
+    if (after + 1 > shadow_chain_slots(s->ch) || after > 4 * std::max<int64_t>(s->built_n, 64)) {
+        s->last = s->B;  // rebuilt from B (a pending commit step is then moot)
+        s->last_phi = s->phiB;
+        s->last_ptS = s->ptSB;
+        s->have_last = true;
+        int rc = build_shadow(ctx, s);
+        if (rc) return rc;
+        nsteps = 0;
+    }
+    e2.decision = 0;
+    steps[nsteps++] = e2;
+    s->ptSQ.assign((size_t)n, 0.0);
+    int rc = shadow_chain_script(s->ch, steps, nsteps, &s->phiQ, s->ptSQ.data());
+    if (rc) {
+        drop_chain(s);
+        s->have_last = false;
+        return rc;
+    }
+    s->e = e2;
+    s->pending = true;
+    return out(s->phiQ, s->ptSQ);
+}
+
+}  // namespace tdstar
