@@ -248,6 +248,7 @@ def main():
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
     if rank == 0 and not a.no_full_evaluate:
         out["full_evaluate"] = full_evaluate(tt, ctx, model, N)
+        out["dropin"] = dropin(tt, ds, model)
     if rank == 0 and not a.no_stress:
         out["stress"] = stress(tt)
     if rank == 0 and a.config4:
@@ -323,6 +324,40 @@ def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3):
             "ms_per_launch": round(kms / max(launches, 1), 4), "iters_per_launch": iters, "roofline": roof}
 
 
+def dropin(tt, ds, model, iters=1500, host_iters=300):
+    """The drop-in boundary as an unchanged Julia host drives it: the
+    reference's loop on the host (TD_inversion_function.jl:70-274), one
+    td_evaluate of the proposed model per proposal and a td_interpolate per
+    birth/death query (:81, :146) -- TD_ENGINE_DROPIN, whose td_evaluate calls
+    take the incremental path -- beside the same loop with every evaluate in
+    full (TD_ENGINE_HOST, what td_evaluate cost before the incremental path)."""
+    prm = tt.define_TDstructrure().replace(max_cells=2 * len(model.xCell))
+    out = {}
+    for name, engine, k in (("incremental", tt.TD_ENGINE_DROPIN, iters), ("full_evaluate", tt.TD_ENGINE_HOST,
+                                                                          host_iters)):
+        ctx = tt.TdContext.from_datastruct(ds)
+        ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000, chain=1, engine=engine), model)
+        ch.run(50)
+        e0 = ch.stats()["evaluations"]
+        ctx.timing(enable=True, reset=True)
+        t0 = time.perf_counter()
+        ch.run(k)
+        el = time.perf_counter() - t0
+        ne = ch.stats()["evaluations"] - e0
+        res = {"proposals_per_s": round(k / el, 1), "us_per_proposal": round(el / k * 1e6, 2), "evaluates": ne,
+               "proposals": k}
+        if engine == tt.TD_ENGINE_DROPIN:
+            nl, ms = ctx.timing(kernel="chain_script")
+            res["script_kernel_us"] = round(ms * 1e3 / max(nl, 1), 2)
+            res["script_launches"] = nl
+        ctx.timing(enable=False)
+        out[name] = res
+        ch.close()
+        ctx.close()
+    out["speedup"] = round(out["incremental"]["proposals_per_s"] / out["full_evaluate"]["proposals_per_s"], 2)
+    return out
+
+
 def full_evaluate(tt, ctx, model, N, reps=50):
     """The drop-in td_evaluate (MCsub.jl:123-185) on the same model, both
     nearest-cell methods: the bucket grid (default from 256 cells) and the
@@ -333,6 +368,7 @@ def full_evaluate(tt, ctx, model, N, reps=50):
     out = {}
     kernels = {"grid": ["nn_grid_build", "nn_grid", "ray_sums_chi2"],
                "brute_force": ["nn_partial", "nn_merge", "ray_sums_chi2"]}
+    tt.lib().tdt_set_incremental(ctx.h, 0)  # every call a full evaluate (repeats would hit the shadow's cache)
     for name, method in (("grid", ctx.NN_GRID), ("brute_force", ctx.NN_BRUTE)):
         ctx.set_nn_method(method)
         for _ in range(3):
@@ -352,6 +388,7 @@ def full_evaluate(tt, ctx, model, N, reps=50):
         out[name] = {"evaluate_ms": round(el * 1e3, 4), "evaluates_per_s": round(1.0 / el, 1),
                      "nn_pair_evals_per_s_equiv": round(E / el, 1), "kernel_ms": km}
     ctx.set_nn_method(ctx.NN_AUTO)
+    tt.lib().tdt_set_incremental(ctx.h, 1)
     t_nn = out["brute_force"]["kernel_ms"]["nn_partial"] / 1e3
     flops = 8.0 * E  # 3 sub + 3 mul + 2 add per distance, no FMA allowed
     tf = flops / t_nn / 1e12 if t_nn > 0 else 0.0

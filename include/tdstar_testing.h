@@ -88,9 +88,19 @@ int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, dou
  * the reference's own model.jld phi values.  1 <= n <= 4096.  Needs a GPU. */
 int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]);
 
-/* td_evaluate's incremental path on (1, default) or off (0: every call is a
- * full evaluate; the shadow chain is released). */
+/* td_evaluate's incremental path: 0 off (every call a full evaluate), 1 one
+ * k_chain_run launch per call, 2 (default) a resident launch fed through a
+ * pinned-memory mailbox (it returns by itself after 200 ms without a call).
+ * Changing the mode releases the shadow chain. */
 int tdt_set_incremental(td_ctx *ctx, int on);
+
+/* Diagnostic of the resident server (mode 2): out = {shader cycles, 100 MHz
+ * wall ticks} of its last evaluation (command receipt to answer), the polls of
+ * the mailbox before that command arrived, 0. */
+int tdt_shadow_diag(td_ctx *ctx, int64_t out[4]);
+/* Diagnostic: stop the resident server and read its chain's phase stamps (as
+ * tdt_chain_profile; stamps are on only with TD_SHADOW_PROFILE set). */
+int tdt_shadow_profile(td_ctx *ctx, int64_t out[80]);
 
 /* Nearest-cell method of td_evaluate / td_interpolate: 0 auto (bucket grid
  * from 256 cells on), 1 brute force (every point x every cell), 2 bucket grid.

@@ -87,6 +87,8 @@ SIGNATURES = {
                                             ctypes.POINTER(ctypes.c_int64), _pi32]),
     "tdt_wave_seq_sum": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _d, _pd, _pd, _pi32]),
     "tdt_set_incremental": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "tdt_shadow_diag": (ctypes.c_int, [_vp, _pi64]),
+    "tdt_shadow_profile": (ctypes.c_int, [_vp, _pi64]),
     "tdt_chi2": (ctypes.c_int, [_vp, _pd, ctypes.c_int, _pd]),
     "tdt_accept": (ctypes.c_int, [ctypes.POINTER(TdChainParams), ctypes.c_int, _d, _d, _i64, _d, _d, _d, _d, _d]),
 }

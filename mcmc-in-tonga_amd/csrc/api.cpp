@@ -451,6 +451,12 @@ int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const 
         return set_err(ctx, TD_ERR_BOUNDS, "td_interpolate: Y/Z shorter than npoints (Julia BoundsError)");
     if (np == 0) return TD_OK;
     TD_HIP(ctx, hipSetDevice(ctx->device));
+    if (np == 1 && !nearest_out && ctx->incremental && nCells > 0) {  // a chain's 1-point query (:81, :146)
+        int handled = 0;
+        int rc = interpolate_incremental(ctx, xCell, yCell, zCell, zeta, nCells, X[0], Y[0], Z[0], zeta_out, &handled);
+        if (rc) return rc;
+        if (handled) return TD_OK;
+    }
     if (np > ctx->q_cap) {
         void *dev[] = {ctx->q, ctx->q_i, ctx->q_z};
         for (void *p : dev)
@@ -607,9 +613,9 @@ int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]) {
 }
 
 int tdt_set_incremental(td_ctx *ctx, int on) {
-    if (!ctx || on < 0 || on > 1) return TD_ERR_ARG;
+    if (!ctx || on < 0 || on > 2) return TD_ERR_ARG;
+    if (on != ctx->incremental) shadow_free(ctx);
     ctx->incremental = on;
-    if (!on) shadow_free(ctx);
     return TD_OK;
 }
 

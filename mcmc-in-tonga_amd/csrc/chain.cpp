@@ -10,7 +10,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -42,6 +46,13 @@ struct td_chain {
     ChainScalars *st_host = nullptr;  // pinned
     NNWork nn;
     double *script_host = nullptr;  // pinned, mapped: [phi_n, ptS_n] of a scripted step (shadow chains)
+    double *script_dev = nullptr;   // the same, as the device addresses it
+    bool desc_dirty = true;         // dev changed on the host since the device copy was made
+    // server mode (shadow chains): the resident launch and its mailbox
+    Mailbox *mb_host = nullptr, *mb_dev = nullptr;
+    hipStream_t srv_stream = nullptr;
+    bool srv_running = false;
+    std::chrono::steady_clock::time_point srv_last{};
 };
 
 namespace {
@@ -440,8 +451,13 @@ int device_pull_scalars(td_chain *ch) {
     return TD_OK;
 }
 
+int server_stop(td_chain *ch);
+
 void free_chain(td_chain *ch) {
     if (!ch) return;
+    (void)server_stop(ch);
+    if (ch->srv_stream) (void)hipStreamDestroy(ch->srv_stream);
+    if (ch->mb_host) (void)hipHostFree(ch->mb_host);
     if (ch->ctx && ch->ctx->stream) (void)hipStreamSynchronize(ch->ctx->stream);
     if (ch->dev_block) (void)hipFree(ch->dev_block);
     if (ch->st_host) (void)hipHostFree(ch->st_host);
@@ -449,6 +465,70 @@ void free_chain(td_chain *ch) {
     if (ch->nn.part_d) (void)hipFree(ch->nn.part_d);
     if (ch->nn.part_i) (void)hipFree(ch->nn.part_i);
     delete ch;
+}
+
+// ---- server mode: one resident k_chain_run per shadow chain, fed through a
+//      mailbox in pinned host memory (chain_dev.h Mailbox) ----
+volatile long long *vol(long long *p) { return p; }
+
+int server_stop(td_chain *ch) {
+    if (!ch || !ch->srv_running) return TD_OK;
+    Mailbox *m = ch->mb_host;
+    if (!*vol(&m->exited)) {
+        m->type = kCmdQuit;
+        std::atomic_thread_fence(std::memory_order_release);
+        *vol(&m->seq) = m->seq + 1;
+    }
+    hipError_t e = hipStreamSynchronize(ch->srv_stream);  // the kernel returns (QUIT, or its idle watchdog)
+    ch->srv_running = false;
+    if (e != hipSuccess) return hip_err(ch->ctx, e, "chain server exit");
+    adopt_scalars(ch);
+    return TD_OK;
+}
+
+int server_start(td_chain *ch) {
+    if (ch->srv_running) return TD_OK;
+    td_ctx *c = ch->ctx;
+    Mailbox *m = ch->mb_host;
+    m->exited = 0;
+    m->done = m->seq;
+    std::atomic_thread_fence(std::memory_order_release);
+    hipError_t e = hipSuccess;
+    if (ch->desc_dirty) {
+        e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, ch->srv_stream);
+        if (e != hipSuccess) return hip_err(c, e, "server descriptor upload");
+        ch->desc_dirty = false;
+    }
+    ScriptArgs sa{};
+    sa.out = ch->script_dev;
+    sa.mb = ch->mb_dev;
+    e = chain_run(&ch->dev, ch->dev_ptr, 1, LLONG_MAX, ch->srv_stream, &sa);
+    if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (server)");
+    ch->srv_running = true;
+    ch->srv_last = std::chrono::steady_clock::now();
+    return TD_OK;
+}
+
+// Post the command already written into the mailbox and wait for its answer.
+int server_post(td_chain *ch) {
+    Mailbox *m = ch->mb_host;
+    const long long sq = m->seq + 1;
+    std::atomic_thread_fence(std::memory_order_release);
+    *vol(&m->seq) = sq;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long long spin = 0;; ++spin) {
+        if (*vol(&m->done) == sq) break;
+        if (*vol(&m->exited)) {  // returned before answering (it was idle past its watchdog)
+            (void)hipStreamSynchronize(ch->srv_stream);
+            ch->srv_running = false;
+            return set_err(ch->ctx, TD_ERR_HIP, "chain server returned before answering");
+        }
+        if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20))
+            return set_err(ch->ctx, TD_ERR_HIP, "chain server: no answer in 20 s");
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    ch->srv_last = std::chrono::steady_clock::now();
+    return TD_OK;
 }
 
 }  // namespace
@@ -532,8 +612,11 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
     }
     Timer *tm = ch->ctx->timer.on ? &ch->ctx->timer : nullptr;
     hipEvent_t t0 = tm ? tm->begin(ch->ctx->stream) : nullptr;
-    e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, ch->ctx->stream);
-    if (e != hipSuccess) return hip_err(ch->ctx, e, "chain descriptor upload");
+    if (ch->desc_dirty) {  // the device copy of the descriptor is current otherwise
+        e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, ch->ctx->stream);
+        if (e != hipSuccess) return hip_err(ch->ctx, e, "chain descriptor upload");
+        ch->desc_dirty = false;
+    }
     e = chain_run(&ch->dev, ch->dev_ptr, 1, iterations, ch->ctx->stream);
     if (tm) tm->end("chain_run", t0, ch->ctx->stream);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "k_chain_run launch");
@@ -643,6 +726,7 @@ int td_chain_set_temperature(td_chain *ch, double temperature) {
     ch->P.temperature = temperature;
     tdchain::params_derived(ch->P);
     ch->dev.params = ch->P;
+    ch->desc_dirty = true;
     return TD_OK;
 }
 
@@ -668,9 +752,17 @@ int shadow_chain_create(td_ctx *ctx, const double *x, const double *y, const dou
     td_chain *ch = nullptr;
     int rc = td_chain_create(&ch, ctx, &p, x, y, z, zeta, ncells);
     if (rc) return rc;
-    hipError_t e = hipHostMalloc(&ch->script_host, sizeof(double) * ((size_t)ctx->g.n + 1),
+    hipError_t e = hipHostMalloc(&ch->script_host, sizeof(double) * ((size_t)ctx->g.n + 2),
                                  hipHostMallocMapped | hipHostMallocCoherent);
-    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&ch->dev.script_out), ch->script_host, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&ch->script_dev), ch->script_host, 0);
+    if (e == hipSuccess)
+        e = hipHostMalloc(&ch->mb_host, sizeof(Mailbox), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+        std::memset(ch->mb_host, 0, sizeof(Mailbox));
+        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&ch->mb_dev), ch->mb_host, 0);
+    }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ch->srv_stream, hipStreamNonBlocking);
+    if (std::getenv("TD_SHADOW_PROFILE")) ch->dev.profile = 1;  // diagnostic phase stamps (tdt_shadow_profile)
     if (e != hipSuccess) {
         free_chain(ch);
         return hip_err(ctx, e, "hipHostMalloc(shadow output)");
@@ -683,32 +775,127 @@ int64_t shadow_chain_slots(const td_chain *ch) { return ch->dev.cap; }
 int64_t shadow_chain_ncells(const td_chain *ch) { return ch->stats.ncells; }
 double shadow_chain_phi(const td_chain *ch) { return ch->phi; }
 
+// The kernel's report [phi, k, (ray, ptS) x k] (k = -1: the whole ptS
+// follows) over the model's ptS `base` -> phi, the proposed model's ptS.
+void unpack_report(const double *buf, int64_t n, const double *base, double *phi, double *ptS) {
+    if (phi) *phi = buf[0];
+    if (!ptS || n == 0) return;
+    const long long k = (long long)buf[1];
+    if (k < 0) {
+        std::memcpy(ptS, buf + 2, sizeof(double) * (size_t)n);
+        return;
+    }
+    std::memcpy(ptS, base, sizeof(double) * (size_t)n);
+    for (long long i = 0; i < k; ++i) ptS[(size_t)buf[2 + 2 * i]] = buf[3 + 2 * i];
+}
+
 // Run 1..kMaxScript host-given steps in one k_chain_run launch; the step with
 // decision 0 (the last) leaves [phi_n, ptS_n] in the pinned output.
-int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, double *phi_out, double *ptS_out) {
+int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, const double *base_ptS, double *phi_out,
+                        double *ptS_out) {
     td_ctx *c = ch->ctx;
     if (nsteps < 1 || nsteps > kMaxScript) return set_err(c, TD_ERR_ARG, "shadow script");
-    ch->dev.nscript = nsteps;
-    for (int k = 0; k < nsteps; ++k) ch->dev.script[k] = steps[k];
+    ScriptArgs sa{};
+    sa.n = nsteps;
+    for (int k = 0; k < nsteps; ++k) sa.step[k] = steps[k];
+    sa.out = ch->script_dev;
     Timer *tm = c->timer.on ? &c->timer : nullptr;
     hipEvent_t t0 = tm ? tm->begin(c->stream) : nullptr;
-    hipError_t e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, c->stream);
-    ch->dev.nscript = 0;
-    if (e != hipSuccess) return hip_err(c, e, "shadow descriptor upload");
-    e = chain_run(&ch->dev, ch->dev_ptr, 1, nsteps, c->stream);
+    hipError_t e = hipSuccess;
+    if (ch->desc_dirty) {
+        e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) return hip_err(c, e, "shadow descriptor upload");
+        ch->desc_dirty = false;
+    }
+    e = chain_run(&ch->dev, ch->dev_ptr, 1, nsteps, c->stream, &sa);
     if (tm) tm->end("chain_script", t0, c->stream);
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (script)");
     e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run (script)");
     adopt_scalars(ch);
     if (steps[nsteps - 1].decision == 0) {
-        if (phi_out) *phi_out = ch->script_host[0];
-        if (ptS_out && c->g.n) std::memcpy(ptS_out, ch->script_host + 1, sizeof(double) * (size_t)c->g.n);
+        unpack_report(ch->script_host, c->g.n, base_ptS, phi_out, ptS_out);
     }
     return TD_OK;
 }
 
+int shadow_chain_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val) {
+    td_ctx *c = ch->ctx;
+    hipError_t e = hipSuccess;
+    if (ch->desc_dirty) {
+        e = hipMemcpyAsync(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) return hip_err(c, e, "shadow descriptor upload");
+        ch->desc_dirty = false;
+    }
+    Timer *tm = c->timer.on ? &c->timer : nullptr;
+    hipEvent_t t0 = tm ? tm->begin(c->stream) : nullptr;
+    e = chain_query(ch->dev_ptr, x, y, z, edit, ch->script_dev, c->stream);
+    if (tm) tm->end("chain_query", t0, c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "k_chain_query launch");
+    e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_err(c, e, "k_chain_query");
+    *val = ch->script_host[0];
+    return TD_OK;
+}
+
 void shadow_chain_destroy(td_chain *ch) { free_chain(ch); }
+
+// Server mode.  Alive: running and used recently (the kernel's own watchdog is
+// 200 ms of silence; past 100 ms the host stops it first, so no command races
+// the watchdog); a stopped server leaves no proposal pending.
+bool shadow_server_alive(td_chain *ch) {
+    if (!ch->srv_running) return false;
+    if (*vol(&ch->mb_host->exited) ||
+        std::chrono::steady_clock::now() - ch->srv_last > std::chrono::milliseconds(100)) {
+        (void)server_stop(ch);
+        return false;
+    }
+    return true;
+}
+
+int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,
+                       double *phi_out, double *ptS_out) {
+    if (nsteps < 1 || nsteps > kMaxScript) return set_err(ch->ctx, TD_ERR_ARG, "server steps");
+    int rc = server_start(ch);
+    if (rc) return rc;
+    Mailbox *m = ch->mb_host;
+    m->type = kCmdEval;
+    m->decision = decision;
+    m->nsteps = nsteps;
+    for (int k = 0; k < nsteps; ++k) m->step[k] = steps[k];
+    rc = server_post(ch);
+    if (rc) return rc;
+    unpack_report(ch->script_host, ch->ctx->g.n, base_ptS, phi_out, ptS_out);
+    return TD_OK;
+}
+
+int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val) {
+    int rc = server_start(ch);
+    if (rc) return rc;
+    Mailbox *m = ch->mb_host;
+    m->type = kCmdQuery;
+    m->q[0] = x;
+    m->q[1] = y;
+    m->q[2] = z;
+    m->has_edit = edit ? 1 : 0;
+    if (edit) m->qedit = *edit;
+    rc = server_post(ch);
+    if (rc) return rc;
+    *val = m->qval;
+    return TD_OK;
+}
+
+int shadow_server_stop(td_chain *ch) { return server_stop(ch); }
+
+int shadow_profile(td_chain *ch, int64_t out[80]) {
+    int rc = server_stop(ch);
+    if (rc) return rc;
+    return tdt_chain_profile(ch, 1, out);
+}
+
+void shadow_server_diag(const td_chain *ch, int64_t out[4]) {
+    for (int k = 0; k < 4; ++k) out[k] = ch->mb_host ? ch->mb_host->diag[k] : 0;
+}
 
 }  // namespace tdstar
 
@@ -745,6 +932,7 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
 int tdt_chain_set_lds_mode(td_chain *ch, int mode) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE || mode < 0 || mode > 1) return TD_ERR_ARG;
     ch->dev.lds_mode = mode;
+    ch->desc_dirty = true;
     return TD_OK;
 }
 
@@ -757,6 +945,7 @@ int tdt_chain_lds(td_chain *ch, int64_t out[4]) {
 int tdt_chain_profile(td_chain *ch, int enable, int64_t out[80]) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE) return TD_ERR_ARG;
     ch->dev.profile = enable;
+    ch->desc_dirty = true;
     if (out) {
         ChainScalars s{};
         hipError_t e = hipMemcpy(&s, ch->st_dev, sizeof s, hipMemcpyDeviceToHost);

@@ -111,12 +111,46 @@ struct DevChain {
     int *bucket_count;      // [G]
     BucketEntry *buckets;   // [G * kBucketCap]
     int *grid_overflow;     // sticky: a bucket overflowed -> always scan all cells
-    // scripted launches (nscript > 0: iteration k runs script[k] instead of a draw;
-    // no early rejection, the decision is the step's): a step with decision 0 writes
-    // [phi_n, ptS_n[0..n)] to script_out (pinned host memory, device address)
-    int nscript;
-    ScriptStep script[kMaxScript];
-    double *script_out;
+};
+
+// Scripted launches (n > 0: iteration k runs step[k] instead of a draw; no
+// early rejection, the decision is the step's): a step with decision 0 writes
+// [phi_n, ptS_n[0..n)] to out (pinned host memory, device address).  Passed
+// by value as a kernel argument: no descriptor copy per call.
+// Server mode (mb != nullptr): the launch stays resident and takes its steps
+// from a mailbox in pinned host memory (td_evaluate's incremental path,
+// incremental.cpp): no launch, no preamble per call.  A step with decision
+// kDecideLater is evaluated, reported (out, done = seq) and its fate taken from
+// the NEXT command; one-point Interpolation queries are answered while it
+// waits.  The kernel returns on QUIT, or by itself after kServerIdleTicks of
+// silence (the pending proposal undone) -- no host, no spinning CU.
+constexpr int kDecideLater = 2;
+enum ServerCmd : int { kCmdEval = 1, kCmdQuery = 2, kCmdQuit = 3 };
+constexpr long long kServerIdleTicks = 20000000;  // 200 ms of the 100 MHz wall clock
+
+struct Mailbox {
+    // host -> device (seq written last)
+    long long seq;
+    int type;        // ServerCmd
+    int decision;    // kCmdEval: the pending proposal's fate (1 commit, 0 undo)
+    int nsteps;      // kCmdEval: steps (the last one kDecideLater)
+    int has_edit;    // kCmdQuery: on the committed model plus qedit
+    ScriptStep step[kMaxScript];
+    double q[3];
+    ScriptStep qedit;
+    // device -> host
+    long long done;    // seq of the last command answered
+    long long exited;  // the kernel has returned (its state is written back)
+    double qval;
+    long long diag[4];  // diagnostic: shader cycles and 100 MHz ticks of the last busy interval, polls
+};
+
+struct ScriptArgs {
+    int n;
+    int pin;  // >= 0: the chain runs on the workgroup that lands on this XCD (L2 kept warm across launches)
+    ScriptStep step[kMaxScript];
+    double *out;
+    Mailbox *mb;  // server mode (device address of pinned host memory)
 };
 
 // Build the cache from scratch for the cells currently in slots 0..ncells-1
@@ -125,7 +159,8 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
 // Run `iters` iterations of `nchains` chains, one persistent workgroup each
 // (workgroup b runs chain b).  `host` = the descriptors, `dev` = their device
 // copy, contiguous (the kernel reads its fields from global memory).
-hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s);
+hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s,
+                     const ScriptArgs *script = nullptr);
 // Testing: the chain's chi^2 code on a caller-given ptS (n <= 4096) --
 // path 2: k_chi2_prefix (the starting state's sequential prefix sums, what
 // chain_full_state runs), 3: the proposal-time sum (the terms of MCsub.jl:171,
@@ -138,11 +173,26 @@ hipError_t test_chain_chi2(const double *ptS, const double *tS, const double *si
 // draws -- it takes the caller's edits as scripted steps (ScriptStep).
 int shadow_chain_create(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                         int64_t ncells, int64_t cap, const double box[6], td_chain **out);
-int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, double *phi_out, double *ptS_out);
+// base_ptS: ptS of the model the last step edits (the report carries the changed rays only)
+int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, const double *base_ptS, double *phi_out,
+                        double *ptS_out);
 int64_t shadow_chain_slots(const td_chain *ch);
 int64_t shadow_chain_ncells(const td_chain *ch);
 double shadow_chain_phi(const td_chain *ch);
 void shadow_chain_destroy(td_chain *ch);
+// server mode (a resident launch fed by a mailbox): decision = the pending proposal's fate
+bool shadow_server_alive(td_chain *ch);
+int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,
+                       double *phi_out, double *ptS_out);
+int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val);
+int shadow_server_stop(td_chain *ch);
+void shadow_server_diag(const td_chain *ch, int64_t out[4]);
+int shadow_profile(td_chain *ch, int64_t out[80]);
+// One-point Interpolation against the chain's model (edit == NULL) or that
+// model plus one edit; *out (device-visible) receives the value.
+hipError_t chain_query(const DevChain *dev, double x, double y, double z, const ScriptStep *edit, double *out,
+                       hipStream_t s);
+int shadow_chain_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val);
 // LDS bytes of the two layouts, whether super-tiles fit, and the layout chain_run takes.
 void chain_lds_sizes(const DevChain &d, int64_t out[4]);
 

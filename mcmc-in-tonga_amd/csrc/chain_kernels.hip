@@ -30,6 +30,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstddef>
+#include <cstdlib>
 
 #include "chain_dev.h"
 #include "exact_sum.h"
@@ -179,6 +181,12 @@ struct Shared {
     double q_zeta;         // result of the birth/death Interpolation query
     int grid_fallbacks32;  // grid searches that needed the full scan
     int grid_ovf;          // LDS copy of *d.grid_overflow
+    // scripted / server steps: the current step, a server command's steps
+    ScriptStep step_cur;
+    ScriptStep srv_step[kMaxScript];
+    int srv_n, srv_k, srv_quit;
+    long long srv_seq, srv_busy_c, srv_busy_w;
+    long long mbox[32];  // server mode: the last command read from the mailbox
     OrphanRec orph[kOrphanLds];
     DeltaSegs dseg;  // rays in HBM: phase F's new chi^2 partial sums as segments over the old ones
     long long prof[kProfSlots], t_last, t_iter;  // diagnostic phase stamps
@@ -541,10 +549,146 @@ __device__ __forceinline__ float f32_up(double x) {
     return (double)f < x ? __int_as_float(__float_as_int(f) + 1) : f;  // f >= 0 finite: the next float up
 }
 
+// dst[0..count) = src[0..count), the whole block: U loads in flight per thread
+// before any store (one memory round trip per U * kChainThreads elements --
+// the launch preamble is latency-bound, not bandwidth-bound)
+template <class T>
+__device__ __forceinline__ void block_copy(T *dst, const T *__restrict__ src, int count, int tid) {
+    constexpr int U = 8;
+    for (int b = tid; b < count; b += U * kChainThreads) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[min(b + u * kChainThreads, count - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (b + u * kChainThreads < count) dst[b + u * kChainThreads] = v[u];
+    }
+}
+
+// System-scope access to the mailbox (pinned host memory, the host polls it)
+__device__ __forceinline__ long long mb_load(const long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void mb_store(long long *p, long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Server mode, wave 0: wait for the next EVAL or QUIT command, answering
+// QUERY commands (one-point Interpolation on the committed model or the model
+// plus one edit -- the state here is the committed one, a pending proposal
+// lives only in the candidate overlay) meanwhile.  EVAL: its steps into
+// sh.srv_*, the pending proposal's fate into sh.accept; QUIT or silence:
+// sh.srv_quit (and undo).
+__device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shared &sh, int lane) {
+    constexpr int kWords = (int)(offsetof(Mailbox, done) / sizeof(long long));
+    static_assert(kWords <= 64 && kWords <= (int)(sizeof(sh.mbox) / sizeof(long long)), "mailbox payload");
+    long long seen = sh.srv_seq;
+    long long t0 = (long long)wall_clock64();
+    if (lane == 0 && sh.srv_busy_c) {  // diagnostic: the busy interval that ends here (clock rate)
+        mb_store(&mb->diag[0], clock64() - sh.srv_busy_c);
+        mb_store(&mb->diag[1], t0 - sh.srv_busy_w);
+    }
+    long long polls = 0;
+    while (true) {
+        const long long sq = mb_load(&mb->seq);
+        ++polls;
+        if (sq != seen) {
+            seen = sq;
+            if (lane == 0) {
+                sh.srv_busy_c = clock64();
+                sh.srv_busy_w = (long long)wall_clock64();
+                mb_store(&mb->diag[2], polls);
+            }
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            // the whole command in one round trip: one mailbox word per lane, into LDS
+            if (lane < kWords) sh.mbox[lane] = mb_load(reinterpret_cast<const long long *>(mb) + lane);
+            wave_sync_lds();
+            const Mailbox &c = *reinterpret_cast<const Mailbox *>(sh.mbox);
+            if (c.type == kCmdQuery) {
+                const double x = c.q[0], y = c.q[1], z = c.q[2];
+                const bool has_edit = c.has_edit != 0;
+                const ScriptStep e = c.qedit;
+                int skip = -1, moved = -1, slot_k = -1;
+                if (has_edit && e.action != tdchain::kBirth) slot_k = v.ord[e.index];
+                if (has_edit && e.action == tdchain::kDeath) skip = slot_k;  // the reduced model (:132-135)
+                if (has_edit && e.action == tdchain::kMove) moved = slot_k;  // the cell at its new site
+                const Nearest r = wave_nearest(d, v, sh, lane, x, y, z, skip, moved, e.x, e.y, e.z);
+                double val = r.z;
+                if (has_edit && e.action == tdchain::kChange && r.s == slot_k) val = e.zeta;
+                if (has_edit && e.action == tdchain::kBirth) {  // the appended cell wins only strictly (last position)
+                    const double dd = dist2(e.x, e.y, e.z, x, y, z);
+                    if (dd < r.d && dd < kSentinel) val = e.zeta;
+                }
+                if (lane == 0) {
+                    mb_store(reinterpret_cast<long long *>(&mb->qval), __double_as_longlong(val));
+                    __threadfence_system();
+                    mb_store(&mb->done, sq);
+                }
+                wave_sync_lds();
+                t0 = (long long)wall_clock64();
+                continue;
+            }
+            if (lane == 0) {
+                sh.srv_seq = sq;
+                if (c.type == kCmdEval) {
+                    const int ns = min(max(c.nsteps, 1), kMaxScript);
+                    for (int k = 0; k < ns; ++k) sh.srv_step[k] = c.step[k];
+                    sh.srv_n = ns;
+                    sh.srv_k = 0;
+                    sh.accept = c.decision != 0 ? 1 : 0;
+                    sh.srv_quit = 0;
+                } else {  // quit: the pending proposal (if any) is undone
+                    sh.accept = 0;
+                    sh.srv_quit = 1;
+                }
+            }
+            wave_sync_lds();
+            return;
+        }
+        if ((long long)wall_clock64() - t0 > kServerIdleTicks) {  // no host: undo and return
+            if (lane == 0) {
+                sh.accept = 0;
+                sh.srv_quit = 1;
+            }
+            wave_sync_lds();
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// One array of a fused block copy: U elements per thread per round, loaded
+// into registers by load(), written by store().  Several Segs loaded before
+// any is stored keep all their loads in flight at once: the launch preamble
+// is a handful of memory round trips whatever the number of arrays.
+template <class T, int U>
+struct CopySeg {
+    T *dst;
+    const T *src;
+    int n;
+    T v[U];
+    __device__ __forceinline__ void load(int b) {
+        if (n <= 0) return;
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[min(b + u * kChainThreads, n - 1)];
+    }
+    __device__ __forceinline__ void store(int b) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (b + u * kChainThreads < n) dst[b + u * kChainThreads] = v[u];
+    }
+};
+
 template <bool SMALL>
-__global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters) {
+__global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters,
+                                                             ScriptArgs sa) {
     constexpr bool WALK = !SMALL || kSmallWalk;  // chi^2 by the event walk
-    const DevChain &d = dptr[blockIdx.x];  // fields read from memory as needed, not pinned in registers
+    if (sa.pin >= 0) {  // one chain, launched as 8 workgroups: only the one on XCD `pin` runs it
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if ((int)(xcc & 15u) != sa.pin) return;
+    }
+    const DevChain &d = dptr[sa.pin >= 0 ? 0 : blockIdx.x];  // fields read from memory as needed
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Shared &sh = *reinterpret_cast<Shared *>(lds);
     const LdsPlan L = lds_plan(d.ntiles, d.n, d.cap, SMALL);
@@ -554,7 +698,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const tdchain::Params &P = d.params;
     const int n = d.n, NT = d.ntiles;
     const bool prof_on = d.profile != 0;
-    const int nscript = d.nscript;  // > 0: host-given proposals (td_evaluate), iters == nscript
+    const long long t_start = prof_on ? clock64() : 0;  // diagnostic: launch preamble / epilogue (prof[76..79])
+    Mailbox *const mb = sa.mb;  // server mode: resident, steps from the mailbox (iters ignored)
+    const int nscript = mb ? 1 : sa.n;  // > 0: host-given proposals (td_evaluate), iters == nscript
 
     // ---- views: LDS copies of the tile / ray / order arrays when they fit ----
     Views v;
@@ -581,24 +727,24 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         double *p = reinterpret_cast<double *>(lds + L.ptS), *pf = reinterpret_cast<double *>(lds + L.prefix);
         double *t = reinterpret_cast<double *>(lds + L.tS), *sg = reinterpret_cast<double *>(lds + L.sig);
         int *rf = reinterpret_cast<int *>(lds + L.rflag), *od = reinterpret_cast<int *>(lds + L.ord);
-        for (int i = tid; i < 3 * NT; i += kChainThreads) {
-            a[i] = d.tile_lo[i];
-            b[i] = d.tile_hi[i];
-        }
-        for (int i = tid; i < NT; i += kChainThreads) m[i] = d.tile_maxd[i];
-        for (int i = tid; i <= NT; i += kChainThreads) ts[i] = d.tile_start[i];
         int *tr = reinterpret_cast<int *>(lds + L.tray);
-        for (int i = tid; i < NT; i += kChainThreads) tr[i] = d.tile_ray[i];
         v.tray = tr;
-        for (int i = tid; i <= n; i += kChainThreads) ro[i] = d.ray_off[i];
-        for (int i = tid; i < n; i += kChainThreads) {
-            p[i] = d.ptS[i];
-            pf[i] = d.prefix[i];
-            t[i] = d.tS[i];
-            sg[i] = d.sig[i];
-            rf[i] = 0;
+        {  // every mirror in one fused copy (positions >= ncells of the order are written before read)
+            constexpr int U = 4;
+            CopySeg<float, U> c0{a, d.tile_lo, 3 * NT}, c1{b, d.tile_hi, 3 * NT};
+            CopySeg<double, U> c2{m, d.tile_maxd, NT}, c3{p, d.ptS, n}, c4{pf, d.prefix, n}, c5{t, d.tS, n},
+                c6{sg, d.sig, n};
+            CopySeg<int, U> c7{ts, d.tile_start, NT + 1}, c8{tr, d.tile_ray, NT}, c9{ro, d.ray_off, n + 1},
+                c10{od, d.order, d.st->ncells};
+            const int most = max(max(3 * NT, NT + 1), max(n + 1, c10.n));
+            for (int b0 = tid; b0 < most; b0 += U * kChainThreads) {
+                c0.load(b0); c1.load(b0); c2.load(b0); c3.load(b0); c4.load(b0); c5.load(b0);
+                c6.load(b0); c7.load(b0); c8.load(b0); c9.load(b0); c10.load(b0);
+                c0.store(b0); c1.store(b0); c2.store(b0); c3.store(b0); c4.store(b0); c5.store(b0);
+                c6.store(b0); c7.store(b0); c8.store(b0); c9.store(b0); c10.store(b0);
+            }
         }
-        for (int i = tid; i < d.cap; i += kChainThreads) od[i] = d.order[i];
+        for (int i = tid; i < n; i += kChainThreads) rf[i] = 0;
         v.tlo = a; v.thi = b; v.tmaxd = m; v.tstart = ts; v.ray_off = ro; v.ptS = p; v.prefix = pf; v.tS = t;
         v.sig = sg; v.rflag = rf; v.ord = od;
         v.cptS = reinterpret_cast<double *>(lds + L.cptS);
@@ -611,6 +757,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         v.rhit_cap = n;
         __syncthreads();  // ptS, tS, sig mirrored
     }
+    const long long t_mirror = prof_on ? clock64() : 0;
     // chi^2 term of every ray in the current state (MCsub.jl:171), cached: a
     // proposal recomputes only the terms of the rays it changes
     for (int r = tid; r < n; r += kChainThreads) {
@@ -639,6 +786,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.dseg.nseg = 0;
     }
     __syncthreads();
+    const long long t_init = prof_on ? clock64() : 0;
     unsigned long long *smask = reinterpret_cast<unsigned long long *>(lds + L.smask);
     unsigned long long *cmask = reinterpret_cast<unsigned long long *>(lds + L.cmask);
     const int NS = d.nsuper;
@@ -672,10 +820,21 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     if (wv == 0) {
         if (!nscript) draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
         wave_sync_lds();
-        if (lane == 0 && iters > 0) {
-            if (nscript)
-                script_proposal(sh.ps[0], d.script[0], sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz, d.czeta,
+        if (mb) {  // the first command (no proposal pending yet)
+            if (lane == 0) {
+                sh.srv_seq = mb_load(&mb->done);
+                sh.srv_quit = 0;
+                sh.srv_busy_c = 0;
+            }
+            wave_sync_lds();
+            server_wait(mb, d, v, sh, lane);
+        }
+        if (lane == 0 && iters > 0 && !(mb && sh.srv_quit)) {
+            if (nscript) {
+                sh.step_cur = mb ? sh.srv_step[sh.srv_k++] : sa.step[0];
+                script_proposal(sh.ps[0], sh.step_cur, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz, d.czeta,
                                 [&](int pos) { return v.ord[pos]; });
+            }
             else
                 make_proposal(sh.ps[0], P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
                               d.czeta, [&](int pos) { return v.ord[pos]; });
@@ -692,12 +851,22 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     // wave 0 lane 0 decides, commits and proposes: the scalars only it changes
     // live in its registers (LDS copies are written, never read back on its path)
     const long long iter0 = sh.iter;
+    if (prof_on && tid == 0) {
+        const long long t_now = clock64();
+        sh.prof[76] += t_now - t_start;  // preamble: mirrors, terms, draws, 1st proposal
+        if (SMALL) {  // its parts (slots of the rays-in-HBM walk diagnostics, unused in this layout)
+            sh.prof[72] += t_mirror - t_start;
+            sh.prof[73] += t_init - t_mirror;
+            sh.prof[74] += t_now - t_init;
+        }
+    }
     double phi_r = sh.phi;
     int cur_r = 0;
     bool pend_r = false;    // rays in HBM: an accepted proposal's chi^2 partial sums not yet written
     bool pend_sup = false;  // rays in HBM: its super-tiles' maxima not yet refreshed
     int last_action = 0, last_accept = 0;  // tid 0: Model.action / accept of the last iteration
-    for (long long it = 0; it < iters; ++it) {
+    long long it_done = 0;                 // iterations run (server mode: until QUIT)
+    for (long long it = 0; it < iters && !(mb && sh.srv_quit); ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
         if constexpr (WALK) {
             // the previous accepted proposal's partial sums (read again only in phase F,
@@ -982,14 +1151,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // Metropolis-Hastings decision (a proven rejection skips the rest of the sum:
                 // accept() on the exact phi_n would reject too)
                 const bool early = fwd && k0 < n && sh.early_reject;
-                const bool acc = nscript ? d.script[it].decision != 0
+                // a scripted step's decision is given (kDecideLater: by the server's next command;
+                // the grid update below is then staged and applied only if it is a commit)
+                const bool acc = nscript ? sh.step_cur.decision == 1
                                          : !early && tdchain::accept(P, pp, phi_r, phi_n, czeta, zeta_killed,
                                                                      zetanew_death, sh.lnN);
                 acc_r = acc;
                 sh.accept = acc ? 1 : 0;
                 sh.phi_n = phi_n;
                 if (prof_on) sh.prof[67] += clock64() - tF;  // diagnostic: decision taken
-                if (acc) {
+                if (acc || (mb && sh.step_cur.decision == kDecideLater)) {
                     sh.g_op = action == tdchain::kBirth ? 2 : action == tdchain::kDeath ? 1
                               : action == tdchain::kMove ? 3 : 0;
                     sh.g_slot = action == tdchain::kBirth ? new_slot : slot_k;
@@ -999,7 +1170,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.g_nx = pp.x;
                     sh.g_ny = pp.y;
                     sh.g_nz = pp.z;
-                    atomicAdd((unsigned long long *)&sh.accepted[action], 1ull);
+                    if (acc) atomicAdd((unsigned long long *)&sh.accepted[action], 1ull);
                 }
                 if (prof_on && early) atomicAdd((unsigned long long *)&sh.prof[14], 1ull);  // proven rejections
             } else if (tid == 64) {  // the next proposal as if this one were rejected
@@ -1075,10 +1246,35 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             STAMP(5);
             // ================= phase G: commit (or undo) =================
             const int nc = sh.n_changed, nr = sh.n_rays;
-            if (nscript && d.script[it].decision == 0) {  // report phi_n and the proposed model's ptS
-                double *out = d.script_out;
-                for (int r = tid; r < n; r += kChainThreads) out[1 + r] = v.rflag[r] ? v.cptS[r] : v.ptS[r];
-                if (tid == 0) out[0] = sh.phi_n;
+            const int sdec = nscript ? sh.step_cur.decision : 1;
+            if (nscript && sdec != 1 && wv == 0) {
+                // report phi_n and the changed rays' new ptS as [phi, k, (ray, ptS) x k] (the
+                // caller holds the model's ptS); k = -1: the whole proposed ptS follows
+                double *out = sa.out;
+                const bool few = 2 * nr + 2 <= n + 1;
+                if (few) {
+                    for (int i = lane; i < nr; i += 64) {
+                        const int r = v.ray_at(i);
+                        out[2 + 2 * i] = (double)r;
+                        out[3 + 2 * i] = v.cptS[r];
+                    }
+                } else {
+                    for (int r = lane; r < n; r += 64) out[2 + r] = v.rflag[r] ? v.cptS[r] : v.ptS[r];
+                }
+                if (lane == 0) {
+                    out[0] = sh.phi_n;
+                    out[1] = few ? (double)nr : -1.0;
+                }
+            }
+            if (mb && sdec == kDecideLater) {  // answer the command, then its fate comes with the next one
+                if (wv == 0) {
+                    __threadfence_system();
+                    wave_sync_lds();
+                    if (lane == 0) mb_store(&mb->done, sh.srv_seq);
+                    server_wait(mb, d, v, sh, lane);
+                }
+                __syncthreads();
+                if (tid == 0) acc_r = sh.accept != 0;
             }
             if (sh.accept) {
                 const int nt = sh.n_tiles, k0 = sh.k0;
@@ -1164,7 +1360,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         // ===== end of iteration: the next proposal (wave 0; draws refilled every 64) =====
         if (wv == 0) {
             if (prof_on && lane == 0) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
-            if (it + 1 < iters) {
+            if (it + 1 < iters && !(mb && sh.srv_quit)) {
                 if (((it + 1) & 63) == 0 && !nscript) {
                     wave_sync_lds();
                     draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(iter0 + it + 1 + lane));
@@ -1186,9 +1382,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         auto slot_at = [&](int pos) {
                             return (killed >= 0 && pos >= killed) ? d.order_tmp[pos + 1] : v.ord[pos];
                         };
-                        if (nscript)
-                            script_proposal(sh.ps[cur_r], d.script[it + 1], sh.nfree, sh.nslots, d.free_slots, d.cx,
+                        if (nscript) {
+                            sh.step_cur = mb ? sh.srv_step[sh.srv_k++] : sa.step[it + 1];
+                            script_proposal(sh.ps[cur_r], sh.step_cur, sh.nfree, sh.nslots, d.free_slots, d.cx,
                                             d.cy, d.cz, d.czeta, slot_at);
+                        }
                         else
                             make_proposal(sh.ps[cur_r], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots,
                                           d.free_slots, d.cx, d.cy, d.cz, d.czeta, slot_at);
@@ -1206,10 +1404,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             }
         }
         STAMP(13);
+        it_done = it + 1;
         __syncthreads();
         STAMP(6);
     }
 
+    const long long t_loop_end = prof_on ? clock64() : 0;
     if constexpr (WALK) {
         if (pend_r) delta_commit<SMALL ? 1 : 16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
         if constexpr (SMALL) __syncthreads();  // the LDS sums are written back below
@@ -1225,7 +1425,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     }
     if (tid == 0) {
         ChainScalars &s = *d.st;
-        s.iter = iter0 + iters;
+        s.iter = iter0 + it_done;
         s.evaluations += sh.evaluations;
         s.bytes += sh.bytes;
         for (int a = 0; a < 5; ++a) {
@@ -1240,10 +1440,52 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             s.last_action = last_action;
             s.last_accept = last_accept;
         }
+        if (prof_on) {
+            sh.prof[77] += clock64() - t_loop_end;  // epilogue (write-backs, scalars) up to here
+            sh.prof[78] += 1;                        // launches
+        }
         for (int k = 0; k < kProfSlots; ++k) s.prof[k] += sh.prof[k];
         s.prof[15] += sh.grid_fallbacks32;  // diagnostic: unproven grid searches
         if (d.st_host) *d.st_host = s;  // the host's pinned mirror: no copy back per chain
+        if (mb) {
+            __threadfence_system();
+            mb_store(&mb->exited, 1);
+        }
     }
+}
+
+// ------------------------------------------------- one-point queries ----
+// Interpolation at one point (MCsub.jl:306-327 with 1-element X/Y/Z, as the
+// reference's birth and death queries call it, TD_inversion_function.jl:81,
+// 146) against a chain's committed model, or that model plus one edit
+// (td_evaluate's pending proposal, incremental.cpp): one wave, the chain's
+// bucket grid (full scan when unproven), the same lexicographic (distance,
+// Julia position) answer as v_nearest.  out[0] = the value.
+__global__ __launch_bounds__(64) void k_chain_query(const DevChain *__restrict__ dptr, double x, double y, double z,
+                                                   ScriptStep e, int has_edit, double *out) {
+    const DevChain &d = *dptr;
+    __shared__ Shared sh;
+    const int lane = threadIdx.x;
+    if (lane == 0) {
+        sh.grid_ovf = *d.grid_overflow;
+        sh.nslots = d.st->nslots;
+        sh.grid_fallbacks32 = 0;
+    }
+    __syncthreads();
+    Views v{};
+    v.ord = d.order;
+    int skip = -1, moved = -1, slot_k = -1;
+    if (has_edit && e.action != tdchain::kBirth) slot_k = d.order[e.index];
+    if (has_edit && e.action == tdchain::kDeath) skip = slot_k;  // the reduced model (:132-135)
+    if (has_edit && e.action == tdchain::kMove) moved = slot_k;  // the cell at its new site
+    Nearest r = wave_nearest(d, v, sh, lane, x, y, z, skip, moved, e.x, e.y, e.z);
+    double val = r.z;
+    if (has_edit && e.action == tdchain::kChange && r.s == slot_k) val = e.zeta;
+    if (has_edit && e.action == tdchain::kBirth) {  // the appended cell: last position, wins only strictly
+        const double dd = dist2(e.x, e.y, e.z, x, y, z);
+        if (dd < r.d && dd < kSentinel) val = e.zeta;
+    }
+    if (lane == 0) out[0] = val;
 }
 
 // ------------------------------------------------------------ full state ----
@@ -1356,6 +1598,14 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
     return e;
 }
 
+hipError_t chain_query(const DevChain *dev, double x, double y, double z, const ScriptStep *edit, double *out,
+                       hipStream_t s) {
+    ScriptStep e{};
+    if (edit) e = *edit;
+    hipLaunchKernelGGL(k_chain_query, dim3(1), dim3(64), 0, s, dev, x, y, z, e, edit ? 1 : 0, out);
+    return hipGetLastError();
+}
+
 void chain_lds_sizes(const DevChain &d, int64_t out[4]) {
     const LdsPlan a = lds_plan(d.ntiles, d.n, d.cap, true), b = lds_plan(d.ntiles, d.n, d.cap, false);
     out[0] = (int64_t)a.total;      // LDS layout (tiles, rays, order mirrored)
@@ -1364,7 +1614,20 @@ void chain_lds_sizes(const DevChain &d, int64_t out[4]) {
     out[3] = (int64_t)(a.total <= kLdsBudget && d.lds_mode != 1);  // the layout a launch takes: 1 = LDS
 }
 
-hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s) {
+hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s,
+                     const ScriptArgs *script) {
+    ScriptArgs sa{};
+    if (script) sa = *script;
+    sa.pin = -1;
+    static const int pin_env = [] {
+        const char *e = std::getenv("TD_XCC_PIN");
+        return e ? std::atoi(e) : -1;
+    }();
+    int grid = nchains;
+    if (nchains == 1 && pin_env >= 0) {
+        sa.pin = pin_env;
+        grid = 8;
+    }
     // one LDS size for the whole grid: the largest plan of any chain; the
     // small (LDS-mirrored) variant only if every chain fits
     size_t small = 0, big = 0;
@@ -1379,9 +1642,9 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
         hipError_t e = hipFuncSetAttribute((const void *)k_chain_run<true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)small);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_chain_run<true>, dim3(nchains), dim3(kChainThreads), small, s, dev, (long long)iters);
+        hipLaunchKernelGGL(k_chain_run<true>, dim3(grid), dim3(kChainThreads), small, s, dev, (long long)iters, sa);
     } else {
-        hipLaunchKernelGGL(k_chain_run<false>, dim3(nchains), dim3(kChainThreads), big, s, dev, (long long)iters);
+        hipLaunchKernelGGL(k_chain_run<false>, dim3(grid), dim3(kChainThreads), big, s, dev, (long long)iters, sa);
     }
     return hipGetLastError();
 }

@@ -62,7 +62,7 @@ struct td_ctx {
     size_t chain_desc_bytes = 0;
     void *h_chain_desc = nullptr;       // pinned staging of the same
     tdstar::td_shadow *shadow = nullptr;  // td_evaluate's incremental path (incremental.cpp)
-    int incremental = 1;                // 0: td_evaluate always evaluates in full (tdt_set_incremental)
+    int incremental = 2;                // 0 full evaluates; 1 one launch per call; 2 a resident server (tdt_set_incremental)
     std::string err;
 };
 
@@ -101,5 +101,8 @@ int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z
 int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                          int64_t ncells, double *ptS_out, double *phi_out);
 void shadow_free(td_ctx *ctx);
+// td_interpolate of one point on the shadow's model (incremental.cpp); *handled = 0: not applicable.
+int interpolate_incremental(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                            int64_t ncells, double qx, double qy, double qz, double *val, int *handled);
 
 }  // namespace tdstar

@@ -57,7 +57,8 @@ struct td_shadow {
     Cells B;                 // committed model (Julia order), what the shadow chain holds
     double phiB = 0.0;
     std::vector<double> ptSB;
-    bool pending = false;    // Q = B + e evaluated (and undone on the device)
+    bool pending = false;    // Q = B + e evaluated (undone on the device, or held there undecided: dev_pending)
+    bool dev_pending = false;  // server mode: the resident kernel holds e's overlay, awaiting its fate
     ScriptStep e{};
     double phiQ = 0.0;
     std::vector<double> ptSQ;
@@ -79,35 +80,96 @@ bool bits_eq(const double *a, const double *b, int64_t n) {
     return n <= 0 || std::memcmp(a, b, sizeof(double) * (size_t)n) == 0;
 }
 
-// first position where (x, y, z, zeta) differ bit-wise, up to n
-int64_t common_prefix(const double *const in[4], const Cells &b, int64_t n) {
-    const double *base[4] = {b.x.data(), b.y.data(), b.z.data(), b.zeta.data()};
-    int64_t lim = n;
+// A model as the committed cells B plus at most one edit e (e.action 0: B
+// itself), read without materialising it: the proposal Q = B + e costs no copy.
+struct View {
+    const Cells &B;
+    ScriptStep e;
+    double edited[4];  // the edited cell (change / move / birth), field by field
+    View(const Cells &b, const ScriptStep *ed) : B(b), e{} {
+        if (ed) e = *ed;
+        if (e.action == 3 || e.action == 4) {
+            const size_t k = (size_t)e.index;
+            edited[0] = e.action == 4 ? e.x : B.x[k];
+            edited[1] = e.action == 4 ? e.y : B.y[k];
+            edited[2] = e.action == 4 ? e.z : B.z[k];
+            edited[3] = e.action == 3 ? e.zeta : B.zeta[k];
+        } else if (e.action == 1) {
+            edited[0] = e.x, edited[1] = e.y, edited[2] = e.z, edited[3] = e.zeta;
+        }
+    }
+    const double *arr(int a) const { return a == 0 ? B.x.data() : a == 1 ? B.y.data() : a == 2 ? B.z.data() : B.zeta.data(); }
+    int64_t size() const { return B.size() + (e.action == 1 ? 1 : e.action == 2 ? -1 : 0); }
+    // the contiguous run of field a from position j: pointer and length
+    const double *run(int a, int64_t j, int64_t *len) const {
+        const int64_t N = B.size(), k = e.index;
+        switch (e.action) {
+            case 1:
+                if (j < N) { *len = N - j; return arr(a) + j; }
+                *len = 1; return &edited[a];
+            case 2:
+                if (j < k) { *len = k - j; return arr(a) + j; }
+                *len = N - 1 - j; return arr(a) + j + 1;
+            case 3:
+            case 4:
+                if (j < k) { *len = k - j; return arr(a) + j; }
+                if (j == k) { *len = 1; return &edited[a]; }
+                *len = N - j; return arr(a) + j;
+            default:
+                *len = N - j; return arr(a) + j;
+        }
+    }
+};
+
+// in[0..len) == field a of v at [off, off + len)?
+bool range_eq(const double *in, int a, int64_t off, int64_t len, const View &v) {
+    while (len > 0) {
+        int64_t r;
+        const double *p = v.run(a, off, &r);
+        r = std::min(r, len);
+        if (!bits_eq(in, p, r)) return false;
+        in += r, off += r, len -= r;
+    }
+    return true;
+}
+
+// first position where (x, y, z, zeta) differ bit-wise, up to lim
+int64_t common_prefix(const double *const in[4], const View &v, int64_t lim) {
     for (int a = 0; a < 4; ++a) {
         int64_t k = 0;
-        constexpr int64_t kBlk = 64;
-        while (k + kBlk <= lim && bits_eq(in[a] + k, base[a] + k, kBlk)) k += kBlk;
-        while (k < lim && std::memcmp(in[a] + k, base[a] + k, sizeof(double)) == 0) ++k;
+        while (k < lim) {
+            int64_t r;
+            const double *p = v.run(a, k, &r);
+            r = std::min(r, lim - k);
+            int64_t j = 0;
+            constexpr int64_t kBlk = 64;
+            while (j + kBlk <= r && bits_eq(in[a] + k + j, p + j, kBlk)) j += kBlk;
+            while (j < r && std::memcmp(in[a] + k + j, p + j, sizeof(double)) == 0) ++j;
+            k += j;
+            if (j < r) break;
+        }
         lim = k;
     }
     return lim;
 }
 
-// Is `in` (M cells) `base` plus one reference-shaped edit?  0: identical,
-// 1: one edit (in *e, decision unset), -1: neither.
-int classify(const double *const in[4], int64_t M, const Cells &base, ScriptStep *e) {
+// Is `in` (M cells) the model `base` plus one reference-shaped edit?  0:
+// identical, 1: one edit (in *e, decision unset), -1: neither.
+int classify(const double *const in[4], int64_t M, const View &base, ScriptStep *e) {
     const int64_t N = base.size();
     const int64_t p = common_prefix(in, base, std::min(M, N));
     std::memset(e, 0, sizeof *e);
+    auto tail_eq = [&](int64_t from_in, int64_t from_base, int64_t t) {
+        for (int a = 0; a < 4; ++a)
+            if (!range_eq(in[a] + from_in, a, from_base, t, base)) return false;
+        return true;
+    };
+    auto cell_eq = [&](int a, int64_t j) { return range_eq(in[a] + j, a, j, 1, base); };
     if (M == N) {
         if (p == N) return 0;
-        const int64_t t = N - p - 1;  // the rest must be unchanged
-        if (!bits_eq(in[0] + p + 1, base.x.data() + p + 1, t) || !bits_eq(in[1] + p + 1, base.y.data() + p + 1, t) ||
-            !bits_eq(in[2] + p + 1, base.z.data() + p + 1, t) || !bits_eq(in[3] + p + 1, base.zeta.data() + p + 1, t))
-            return -1;
-        const bool site = bits_eq(in[0] + p, base.x.data() + p, 1) && bits_eq(in[1] + p, base.y.data() + p, 1) &&
-                          bits_eq(in[2] + p, base.z.data() + p, 1);
-        const bool val = bits_eq(in[3] + p, base.zeta.data() + p, 1);
+        if (!tail_eq(p + 1, p + 1, N - p - 1)) return -1;  // the rest must be unchanged
+        const bool site = cell_eq(0, p) && cell_eq(1, p) && cell_eq(2, p);
+        const bool val = cell_eq(3, p);
         e->index = (int)p;
         if (site && !val) {  // change (:189)
             if (!std::isfinite(in[3][p])) return -1;
@@ -136,10 +198,7 @@ int classify(const double *const in[4], int64_t M, const Cells &base, ScriptStep
         return 1;
     }
     if (M == N - 1 && M >= 1) {  // death: deleteat!(kill) (:132-135)
-        const int64_t t = M - p;
-        if (!bits_eq(in[0] + p, base.x.data() + p + 1, t) || !bits_eq(in[1] + p, base.y.data() + p + 1, t) ||
-            !bits_eq(in[2] + p, base.z.data() + p + 1, t) || !bits_eq(in[3] + p, base.zeta.data() + p + 1, t))
-            return -1;
+        if (!tail_eq(p, p + 1, M - p)) return -1;
         e->action = 2;
         e->index = (int)p;
         return 1;
@@ -157,6 +216,7 @@ void drop_chain(td_shadow *s) {
     if (s->ch) shadow_chain_destroy(s->ch);
     s->ch = nullptr;
     s->pending = false;
+    s->dev_pending = false;
 }
 
 // Build the shadow chain from the last fully evaluated model.
@@ -218,29 +278,34 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
     };
     if (!s->ch) {
         ScriptStep e;
-        if (!s->have_last || classify(in, M, s->last, &e) < 0) return full();
+        if (!s->have_last || classify(in, M, View(s->last, nullptr), &e) < 0) return full();
         int rc = build_shadow(ctx, s);  // the caller is walking a chain: follow it on the device
         if (rc) return rc;
     }
+    // server mode (incremental == 2): one resident launch answers every call
+    const bool srv = ctx->incremental == 2;
+    if (s->dev_pending && !(srv && shadow_server_alive(s->ch))) s->dev_pending = false;  // stopped: undone
     // which state is the new model an edit of?
     ScriptStep e2;
     ScriptStep steps[kMaxScript];
-    int nsteps = 0;
-    const int rb = classify(in, M, s->B, &e2);
+    int nsteps = 0, decision = 0;  // decision: the fate of the device's pending proposal
+    const int rb = classify(in, M, View(s->B, nullptr), &e2);
     if (rb == 0) return out(s->phiB, s->ptSB);
     if (rb == 1 && s->pending && std::memcmp(&e2, &s->e, sizeof e2) == 0) return out(s->phiQ, s->ptSQ);  // == Q again
     if (rb == 1) {
-        s->pending = false;  // Q (if any) was rejected: it is already undone
+        s->pending = false;  // Q (if any) was rejected: undone (decision 0)
     } else if (s->pending) {
-        Cells Q = s->B;
-        Q.apply(s->e);
-        const int rq = classify(in, M, Q, &e2);
+        const int rq = classify(in, M, View(s->B, &s->e), &e2);
         if (rq < 0) return full();
         if (rq == 0) return out(s->phiQ, s->ptSQ);
-        ScriptStep c = s->e;
-        c.decision = 1;  // Julia went on from Q: commit it first
-        steps[nsteps++] = c;
-        s->B.x.swap(Q.x), s->B.y.swap(Q.y), s->B.z.swap(Q.z), s->B.zeta.swap(Q.zeta);
+        if (s->dev_pending) {
+            decision = 1;  // Julia went on from Q: the device commits its pending overlay
+        } else {
+            ScriptStep c = s->e;
+            c.decision = 1;  // re-evaluate and commit Q first
+            steps[nsteps++] = c;
+        }
+        s->B.apply(s->e);  // B := Q (in place: O(1) but for a death's shift)
         s->phiB = s->phiQ;
         s->ptSB.swap(s->ptSQ);
         s->pending = false;
@@ -259,18 +324,64 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
         if (rc) return rc;
         nsteps = 0;
     }
-    e2.decision = 0;
+    e2.decision = srv ? kDecideLater : 0;
     steps[nsteps++] = e2;
     s->ptSQ.assign((size_t)n, 0.0);
-    int rc = shadow_chain_script(s->ch, steps, nsteps, &s->phiQ, s->ptSQ.data());
+    int rc = srv ? shadow_server_eval(s->ch, decision, steps, nsteps, s->ptSB.data(), &s->phiQ, s->ptSQ.data())
+                 : shadow_chain_script(s->ch, steps, nsteps, s->ptSB.data(), &s->phiQ, s->ptSQ.data());
     if (rc) {
         drop_chain(s);
         s->have_last = false;
         return rc;
     }
+    e2.decision = 0;
     s->e = e2;
     s->pending = true;
+    s->dev_pending = srv;
     return out(s->phiQ, s->ptSQ);
 }
 
+// td_interpolate of ONE point (the reference's birth / death queries,
+// TD_inversion_function.jl:81,146) when the cells are the shadow's committed
+// model or its pending proposal: answered on the device chain's bucket grid.
+// Returns 1 (handled, *val set), 0 (not this context's model: caller takes the
+// plain path) or an error status < 0 never (errors are returned as > 1 codes).
+int interpolate_incremental(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
+                            int64_t M, double qx, double qy, double qz, double *val, int *handled) {
+    *handled = 0;
+    td_shadow *s = ctx->shadow;
+    if (!s || !s->ch || !std::isfinite(qx) || !std::isfinite(qy) || !std::isfinite(qz)) return TD_OK;
+    const double *in[4] = {x, y, z, zeta};
+    ScriptStep e2;
+    const int rb = classify(in, M, View(s->B, nullptr), &e2);
+    const ScriptStep *edit = nullptr;
+    if (rb == 0) {
+        edit = nullptr;  // the committed model
+    } else if (rb == 1 && s->pending && std::memcmp(&e2, &s->e, sizeof e2) == 0) {
+        edit = &s->e;  // the pending proposal (e.g. death's query on modeln, :146)
+    } else {
+        return TD_OK;
+    }
+    if (s->dev_pending && !shadow_server_alive(s->ch)) s->dev_pending = false;
+    // a running server holds the state (its LDS mirrors are not written back): ask it
+    int rc = shadow_server_alive(s->ch) ? shadow_server_query(s->ch, qx, qy, qz, edit, val)
+                                        : shadow_chain_query(s->ch, qx, qy, qz, edit, val);
+    if (rc) return rc;
+    *handled = 1;
+    return TD_OK;
+}
+
 }  // namespace tdstar
+
+extern "C" int tdt_shadow_profile(td_ctx *ctx, int64_t out[80]) {
+    if (!ctx || !out || !ctx->shadow || !ctx->shadow->ch) return TD_ERR_ARG;
+    ctx->shadow->dev_pending = false;  // the server stops: its pending proposal is undone
+    return tdstar::shadow_profile(ctx->shadow->ch, out);
+}
+
+extern "C" int tdt_shadow_diag(td_ctx *ctx, int64_t out[4]) {
+    if (!ctx || !out) return TD_ERR_ARG;
+    for (int k = 0; k < 4; ++k) out[k] = 0;
+    if (ctx->shadow && ctx->shadow->ch) tdstar::shadow_server_diag(ctx->shadow->ch, out);
+    return TD_OK;
+}

@@ -88,12 +88,18 @@ def check(ctx, ref_ctx, cells):
     return a
 
 
-def test_edit_sequences_equal_full_evaluate(tt, ctx, ref_ctx):
+@pytest.mark.parametrize("mode", [2, 1])
+def test_edit_sequences_equal_full_evaluate(tt, ds, ref_ctx, mode):
     """A random walk of edits where the 'host' goes on from the proposal (accept)
     or from the previous model (reject) at random, plus repeats of the same
-    model (prior-2 deaths call evaluate twice, :141,159), unrelated models and
-    a nearest-index request in between."""
-    rng = np.random.default_rng(11)
+    model (prior-2 deaths call evaluate twice, :141,159), unrelated models,
+    a nearest-index request and pauses past the resident server's idle limit
+    in between.  mode 2: the resident server (default); 1: a launch per call."""
+    import time
+
+    ctx = tt.TdContext.from_datastruct(ds)
+    assert tt.lib().tdt_set_incremental(ctx.h, mode) == 0
+    rng = np.random.default_rng(11 + mode)
     box = tt.box()
     cur = tt.random_model(400, 11).cells()
     check(ctx, ref_ctx, cur)
@@ -108,8 +114,19 @@ def test_edit_sequences_equal_full_evaluate(tt, ctx, ref_ctx):
         if 0.5 < r < 0.52:  # nearest indices requested: always the full path
             _, phi, _, near = ctx.evaluate(prop, want_nearest=True)
             assert near is not None and phi == ref_ctx.evaluate(prop)[1]
+        for cells in (prop, cur):  # 1-point Interpolation on the proposal / the model (:81, :146)
+            q = [rng.uniform(box[0], box[1]), rng.uniform(box[2], box[3]), rng.uniform(box[4], box[5])]
+            if rng.random() < 0.3 and len(cells[0]) > 0:  # exactly on a cell: a tie with its duplicate site
+                k = int(rng.integers(len(cells[0])))
+                q = [cells[0][k], cells[1][k], cells[2][k]]
+            a, _ = ctx.interpolate(cells, [q[0]], [q[1]], [q[2]])
+            b, _ = ref_ctx.interpolate(cells, [q[0]], [q[1]], [q[2]])
+            assert np.array_equal(a, b), (step, q)
         if rng.random() < 0.55:
             cur = prop
+        if step % 150 == 149:
+            time.sleep(0.25)  # the server is stopped (host side) / returns by itself; state stays exact
+    ctx.close()
 
 
 def test_adversarial_edits(tt, ctx, ref_ctx):
