@@ -107,6 +107,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full-evaluate", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in leg (td_evaluate called per proposal by a host loop)")
     ap.add_argument("--chains-per-gpu", type=int, default=1,
                     help="independent chains per rank, one workgroup each, one launch (td_chain_run_batch)")
     ap.add_argument("--swap-every", type=int, default=0,
@@ -248,6 +250,7 @@ def main():
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
     if rank == 0 and not a.no_full_evaluate:
         out["full_evaluate"] = full_evaluate(tt, ctx, model, N)
+    if rank == 0 and not a.no_dropin:
         out["dropin"] = dropin(tt, ds, model)
     if rank == 0 and not a.no_stress:
         out["stress"] = stress(tt)
@@ -347,9 +350,8 @@ def dropin(tt, ds, model, iters=1500, host_iters=300):
         res = {"proposals_per_s": round(k / el, 1), "us_per_proposal": round(el / k * 1e6, 2), "evaluates": ne,
                "proposals": k}
         if engine == tt.TD_ENGINE_DROPIN:
-            nl, ms = ctx.timing(kernel="chain_script")
-            res["script_kernel_us"] = round(ms * 1e3 / max(nl, 1), 2)
-            res["script_launches"] = nl
+            res["served_by"] = ("one resident k_chain_run per shadow chain, fed each td_evaluate / td_interpolate "
+                                "through a pinned mailbox (no launch per call)")
         ctx.timing(enable=False)
         out[name] = res
         ch.close()
@@ -367,7 +369,7 @@ def full_evaluate(tt, ctx, model, N, reps=50):
     E = ctx.P * N
     out = {}
     kernels = {"grid": ["nn_grid_build", "nn_grid", "ray_sums_chi2"],
-               "brute_force": ["nn_partial", "nn_merge", "ray_sums_chi2"]}
+               "brute_force": ["nn_tile", "nn_partial", "nn_merge", "ray_sums_chi2"]}
     tt.lib().tdt_set_incremental(ctx.h, 0)  # every call a full evaluate (repeats would hit the shadow's cache)
     for name, method in (("grid", ctx.NN_GRID), ("brute_force", ctx.NN_BRUTE)):
         ctx.set_nn_method(method)
@@ -383,18 +385,28 @@ def full_evaluate(tt, ctx, model, N, reps=50):
         km = {}
         for k in kernels[name]:
             nl, ms = ctx.timing(kernel=k)
-            km[k] = round(ms / max(nl, 1), 4)
+            if nl:
+                km[k] = round(ms / nl, 4)
         ctx.timing(enable=False)
         out[name] = {"evaluate_ms": round(el * 1e3, 4), "evaluates_per_s": round(1.0 / el, 1),
                      "nn_pair_evals_per_s_equiv": round(E / el, 1), "kernel_ms": km}
     ctx.set_nn_method(ctx.NN_AUTO)
     tt.lib().tdt_set_incremental(ctx.h, 1)
-    t_nn = out["brute_force"]["kernel_ms"]["nn_partial"] / 1e3
+    # the dominant kernel: the one-launch tile search where the points fit a lane each per CU, else the
+    # split search (whose merge launch is reported beside it)
+    km = out["brute_force"]["kernel_ms"]
+    kname = "nn_tile" if "nn_tile" in km else "nn_partial"
+    t_nn = km.get(kname, 0.0) / 1e3
     flops = 8.0 * E  # 3 sub + 3 mul + 2 add per distance, no FMA allowed
     tf = flops / t_nn / 1e12 if t_nn > 0 else 0.0
-    out["brute_force"]["roofline"] = {"kernel": "nn_partial", "bound": "valu-fp64", "achieved": round(tf, 3),
+    out["brute_force"]["roofline"] = {"kernel": kname, "bound": "valu-fp64", "achieved": round(tf, 3),
                                       "peak": FP64_NOFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                       "frac": round(tf / FP64_NOFMA_PEAK_TFLOPS, 4), "flops_per_launch": flops}
+    tr, src, _ = measured_traffic("k_%s/config3" % kname) if ctx.P < 100000 else (None, None, None)
+    if tr is not None:
+        out["brute_force"]["roofline"]["traffic"] = tr
+        out["brute_force"]["roofline"]["traffic_source"] = src
+        out["brute_force"]["roofline"]["compulsory_bytes"] = 24 * ctx.P + 32 * N + 20 * ctx.P
     return out
 
 

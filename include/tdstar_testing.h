@@ -103,9 +103,18 @@ int tdt_shadow_diag(td_ctx *ctx, int64_t out[4]);
 int tdt_shadow_profile(td_ctx *ctx, int64_t out[80]);
 
 /* Nearest-cell method of td_evaluate / td_interpolate: 0 auto (bucket grid
- * from 256 cells on), 1 brute force (every point x every cell), 2 bucket grid.
- * All give the same answer (the lexicographic (distance, index) minimum). */
+ * from 256 cells on), 1 brute force (every point x every cell: the one-launch
+ * tile search where the points fit a lane each per CU, else the split search),
+ * 2 bucket grid, 3 brute force through the split search (k_nn_partial +
+ * k_nn_merge) always.  All give the same answer (the lexicographic
+ * (distance, index) minimum). */
 int tdt_set_nn_method(td_ctx *ctx, int method);
+
+/* Diagnostic: the nearest-cell search alone, `reps` back-to-back launches over
+ * the context's ray points on the given cells (method as tdt_set_nn_method,
+ * 1..3), timed by two HIP events; *us_out = microseconds per search. */
+int tdt_nn_bench(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta, int64_t ncells,
+                 int method, int reps, double *us_out);
 
 #ifdef __cplusplus
 }

@@ -612,6 +612,42 @@ int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]) {
     return TD_OK;
 }
 
+int tdt_nn_bench(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta, int64_t ncells,
+                 int method, int reps, double *us_out) {
+    if (!ctx || !us_out || reps < 1 || method < 1 || method > 3 || ncells < 1)
+        return set_err(ctx, TD_ERR_ARG, "tdt_nn_bench");
+    TD_HIP(ctx, hipSetDevice(ctx->device));
+    const int old_m = ctx->nn_method, old_s = ctx->nn.method;
+    ctx->nn_method = method == 2 ? 2 : 1;
+    ctx->nn.method = method == 3 ? kNNSplit : kNNAuto;
+    int rc = upload_cells(ctx, x, y, z, zeta, ncells);
+    const auto &g = ctx->g;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipSuccess;
+    if (!rc) {
+        e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, ncells, ctx->best_i, ctx->best_d, ctx->zeta0);  // warm
+        if (e == hipSuccess) e = hipEventCreate(&e0);
+        if (e == hipSuccess) e = hipEventCreate(&e1);
+        if (e == hipSuccess) e = hipEventRecord(e0, ctx->stream);
+        for (int k = 0; k < reps && e == hipSuccess; ++k) {
+            if (method == 2) ctx->cells_stage = nullptr;  // grid: rebuilt from the device copy each time
+            e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, ncells, ctx->best_i, ctx->best_d, ctx->zeta0);
+        }
+        if (e == hipSuccess) e = hipEventRecord(e1, ctx->stream);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        float ms = 0.f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+        *us_out = (double)ms * 1e3 / reps;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    ctx->nn_method = old_m;
+    ctx->nn.method = old_s;
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_err(ctx, e, "tdt_nn_bench");
+    return TD_OK;
+}
+
 int tdt_set_incremental(td_ctx *ctx, int on) {
     if (!ctx || on < 0 || on > 2) return TD_ERR_ARG;
     if (on != ctx->incremental) shadow_free(ctx);
@@ -620,8 +656,9 @@ int tdt_set_incremental(td_ctx *ctx, int on) {
 }
 
 int tdt_set_nn_method(td_ctx *ctx, int method) {
-    if (!ctx || method < 0 || method > 2) return TD_ERR_ARG;
-    ctx->nn_method = method;
+    if (!ctx || method < 0 || method > 3) return TD_ERR_ARG;
+    ctx->nn_method = method == 3 ? 1 : method;  // 3: brute force through the split search
+    ctx->nn.method = method == 3 ? kNNSplit : kNNAuto;
     return TD_OK;
 }
 

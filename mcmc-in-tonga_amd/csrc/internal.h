@@ -99,6 +99,9 @@ constexpr int kGridCap = 16;               // entries per bucket (a fuller bucke
 constexpr int kGridMinCells = 256;     // below: the brute force is as fast
 
 // Workspace for the nearest searches (split brute force; bucket grid).
+constexpr int kNNAuto = 0;   // brute force: k_nn_tile when the points fit one lane each per CU
+constexpr int kNNSplit = 1;  // brute force: always the split search (k_nn_partial + k_nn_merge)
+
 struct NNWork {
     double *part_d = nullptr;  // [chunks][npts]
     int *part_i = nullptr;
@@ -108,6 +111,7 @@ struct NNWork {
     size_t g_count_cap = 0, g_ent_cap = 0;  // bytes (g_count: both sets)
     int g_par = 0;                 // the set the next search fills (zero)
     int64_t g_used[2] = {0, 0};    // buckets each set holds counts in (zeroed by the other's search)
+    int method = 0;                // brute force: kNNAuto (one-launch tile search where it fits) or kNNSplit
 };
 
 struct Geometry {
@@ -127,6 +131,15 @@ struct NNPlan {
     int chunk;     // cells per chunk (LDS-staged)
 };
 NNPlan plan_nearest(int64_t npts, int64_t ncells, int num_cus);
+
+// The one-launch brute force (k_nn_tile): one workgroup per CU owns Q points
+// and scans every cell for them in S slices of L cells, staged R at a time.
+struct TilePlan {
+    bool ok = false;  // false: too many points per CU, use the split search
+    int Q = 0, S = 0, L = 0, R = 0, blocks = 0, ppl = 2;
+    size_t lds = 0;
+};
+TilePlan plan_tile(int64_t npts, int64_t ncells, int num_cus);
 
 // nearest cell of each point (split search + ordered merge).  cells = SoA
 // (x at [0], y at [stride], z at [2*stride], zeta at [3*stride]).

@@ -64,11 +64,13 @@ class TdContext:
         check(lib().td_get_info(self.h, ctypes.byref(info)), self.h)
         self.likelihood_const = float(info.likelihood)
 
-    NN_AUTO, NN_BRUTE, NN_GRID = 0, 1, 2
+    NN_AUTO, NN_BRUTE, NN_GRID, NN_BRUTE_SPLIT = 0, 1, 2, 3
 
     def set_nn_method(self, method):
         """Nearest-cell search: NN_AUTO (bucket grid from 256 cells on), NN_BRUTE
-        (every point x every cell, the reference's loop), NN_GRID.  Same answer."""
+        (every point x every cell, the reference's loop: one launch of k_nn_tile
+        where it fits), NN_GRID, NN_BRUTE_SPLIT (brute force through k_nn_partial
+        + k_nn_merge).  Same answer."""
         check(lib().tdt_set_nn_method(self.h, int(method)), self.h)
 
     def timing(self, enable=None, reset=False, kernel=None):

@@ -192,7 +192,7 @@ def test_stress_full_size_properties(tt):
 
 def _both_methods(tt, ctx, orc, ds, cells):
     out = []
-    for m in (ctx.NN_BRUTE, ctx.NN_GRID):
+    for m in (ctx.NN_BRUTE, ctx.NN_GRID, ctx.NN_BRUTE_SPLIT):
         ctx.set_nn_method(m)
         out.append(ctx.evaluate(cells, want_nearest=True))
     ctx.set_nn_method(ctx.NN_AUTO)
@@ -243,7 +243,7 @@ def test_grid_interpolate_adversarial(tt, orc, ctx):
     X = np.concatenate([np.arange(-100, 1100, 25.0), rng.uniform(-500, 1500, 300), [np.nan, 5.0]])
     Y = np.concatenate([np.full(48, 50.0), rng.uniform(-500, 800, 300), [0.0, 0.0]])
     Z = np.concatenate([np.arange(0, 48 * 14, 14.0), rng.uniform(-100, 800, 300), [0.0, 0.0]])
-    for m in (ctx.NN_BRUTE, ctx.NN_GRID):
+    for m in (ctx.NN_BRUTE, ctx.NN_GRID, ctx.NN_BRUTE_SPLIT):
         ctx.set_nn_method(m)
         zr, near = ctx.interpolate(cells, X, Y, Z, want_nearest=True)
         ref, ref_ids = orc.interpolation(cells, X, Y, Z)
@@ -264,3 +264,33 @@ def test_many_rays_exact_chi2(tt, orc, ncells):
     assert np.array_equal(ptS, ref["ptS"])
     assert phi == ref["phi"] and lk == ref["likelihood"]
     ctx.close()
+
+
+@pytest.mark.parametrize("npts", [1, 5, 255, 257, 3001, 16845, 70000, 133000])
+def test_tile_brute_force_plans(tt, orc, ctx, npts):
+    """The one-launch brute force (k_nn_tile) over the shapes its plan takes:
+    one point per CU (256 slices), a few points per CU, a full config-3 point
+    set, and a point set past its lane budget (the split search takes over);
+    cell counts below one group of 8, on and off slice / round boundaries,
+    exact ties across slices (duplicated cells) and NaN cells.  Index and
+    value must equal the oracle's v_nearest and the split search."""
+    rng = np.random.default_rng(npts)
+    xmin, xmax, ymin, ymax, zmin, zmax = tt.box()
+    X = rng.uniform(xmin, xmax, npts)
+    Y = rng.uniform(ymin, ymax, npts)
+    Z = rng.uniform(zmin, zmax, npts)
+    for nc in ((1, 7, 8, 9, 333, 1023, 5000) if npts <= 16845 else (5000,)):
+        x, y, z, zeta = (a.copy() for a in tt.random_model(nc, nc + 3).cells())
+        if nc >= 9:  # duplicates far apart in index (different slices), different values
+            k = nc // 3
+            x[-k:], y[-k:], z[-k:] = x[:k], y[:k], z[:k]
+            zeta[-k:] = zeta[:k] + 1.0
+            x[1::37] = np.nan
+        cells = (x, y, z, zeta)
+        ref, ref_ids = orc.interpolation(cells, X, Y, Z)
+        for m in (ctx.NN_BRUTE, ctx.NN_BRUTE_SPLIT):
+            ctx.set_nn_method(m)
+            zr, near = ctx.interpolate(cells, X, Y, Z, want_nearest=True)
+            assert np.array_equal(near, ref_ids), (m, nc, np.flatnonzero(near != ref_ids)[:5])
+            assert np.array_equal(zr, ref), (m, nc)
+    ctx.set_nn_method(ctx.NN_AUTO)
