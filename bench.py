@@ -248,6 +248,10 @@ def main():
     if ladder is not None:
         out["tempering"] = {"replicas": ladder.R, "temps": [round(t, 4) for t in ladder.temps],
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
+    if dist is not None and not a.no_stress:  # every rank: the stress evaluate split over the ranks' rays
+        sh = stress_sharded(tt, tt.Exchange(dist, coll_dev), dist, coll_dev, local)
+        if rank == 0:
+            out["stress_sharded"] = sh
     if rank == 0 and not a.no_full_evaluate:
         out["full_evaluate"] = full_evaluate(tt, ctx, model, N)
     if rank == 0 and not a.no_dropin:
@@ -436,6 +440,36 @@ def stress(tt, chain_iters=2000):
                                                "k_chain_run/stress", chain_iters == 2000)}
     ch.close()
     ctx.close()
+    return res
+
+
+def stress_sharded(tt, ex, dist, coll_dev, device, reps=10):
+    """SURVEY 8e's optional intra-chain split, on config 5's evaluate: every
+    rank owns a ray range of the 10k synthetic rays (sharded.py), one evaluate
+    = td_evaluate of its shard + an allgather of ptS + td_misfit of all rays
+    (bit-identical to one GPU's evaluate: tests/test_gpu_sharded.py).  Full
+    evaluates (no incremental path), time = max over ranks."""
+    import torch
+
+    ds = tt.synthetic_rays(10000, seed=5)
+    sc = tt.RayShardedContext(ds, ex, device=device)
+    tt.lib().tdt_set_incremental(sc.local.h, 0)
+    cells = tt.random_model(20000, 5).cells()
+    for _ in range(2):
+        sc.evaluate(cells)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, phi, _ = sc.evaluate(cells)
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    res = {"ranks": ex.world, "rays": int(sc.n), "cells": 20000, "evaluate_ms": round(el / reps * 1e3, 4),
+           "evaluates_per_s": round(reps / el, 1), "rays_per_rank": [b - a for a, b in sc.bounds], "phi": phi,
+           "note": "td_evaluate of each rank's rays + allgather of ptS + td_misfit (sequential chi^2 of all rays); "
+                   "compare stress.evaluate.grid.evaluate_ms (one GPU, all rays)"}
+    sc.close()
     return res
 
 

@@ -109,6 +109,18 @@ int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const dou
                 const double *zeta, int64_t nCells, int debug_prior, double *ptS_out, double *phi_out,
                 double *likelihood_out, int32_t *nearest_out);
 
+/* The chi^2 and likelihood of MCsub.jl:169-182 for a caller-given ptS of n
+ * rays (tS, allSig: the n data and errors): phi = the sequential
+ * sum_k ((ptS-tS)[k]^2 * 1.0) / allSig[k]^2, computed on the device exactly as
+ * td_evaluate's (bit for bit), and likelihood = the a5 constant in Julia's
+ * sum association.  The reduction step of a ray-sharded evaluate: every rank
+ * td_evaluate's a context over its own ray subset, the ptS are gathered in
+ * ray order (one allgather), and phi is this call on the whole vector
+ * (mcmc-in-tonga_amd/sharded.py).  tS / allSig are re-uploaded only when
+ * they change between calls. */
+int td_misfit(td_ctx *ctx, int64_t n, const double *ptS, const double *tS, const double *allSig, double *phi_out,
+              double *likelihood_out);
+
 /* Several models at once (independent chains / tempering replicas on one
  * GPU): model k's cells are [cell_off[k], cell_off[k+1]) of the cell arrays.
  * ptS_out is nmodels x n (row k = model k), phi_out/likelihood_out nmodels. */

@@ -52,6 +52,7 @@ SIGNATURES = {
     "td_last_error": (ctypes.c_char_p, [_vp]),
     "td_get_info": (ctypes.c_int, [_vp, ctypes.POINTER(TdInfo)]),
     "td_set_sigma": (ctypes.c_int, [_vp, _pd]),
+    "td_misfit": (ctypes.c_int, [_vp, _i64, _pd, _pd, _pd, _pd, _pd]),
     "td_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "td_timing_reset": (ctypes.c_int, [_vp]),
     "td_timing_get": (ctypes.c_int, [_vp, ctypes.c_char_p, _pi64, _pd]),

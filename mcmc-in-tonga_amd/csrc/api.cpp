@@ -222,10 +222,11 @@ void free_ctx(td_ctx *c) {
     c->timer.release();
     void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->g.done, c->cells,
                    c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->phi,
-                   c->q, c->q_i, c->q_z, c->chain_desc, c->nn.g_count, c->nn.g_ent, c->raster, c->raster_i};
+                   c->q, c->q_i, c->q_z, c->chain_desc, c->nn.g_count, c->nn.g_ent, c->raster, c->raster_i,
+                   c->mf_dev};
     for (void *p : dev)
         if (p) (void)hipFree(p);
-    void *host[] = {c->h_cells, c->h_out, c->h_best_i, c->h_q, c->h_q_i, c->h_q_z, c->h_chain_desc};
+    void *host[] = {c->h_cells, c->h_out, c->h_best_i, c->h_q, c->h_q_i, c->h_q_z, c->h_chain_desc, c->mf_host};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -393,6 +394,52 @@ int td_set_sigma(td_ctx *ctx, const double *allSig) {
     ctx->likelihood = likelihood_constant(allSig, ctx->g.n);
     if (ctx->g.n)
         TD_HIP(ctx, hipMemcpy(ctx->g.sig, allSig, sizeof(double) * (size_t)ctx->g.n, hipMemcpyHostToDevice));
+    return TD_OK;
+}
+
+int td_misfit(td_ctx *ctx, int64_t n, const double *ptS, const double *tS, const double *allSig, double *phi_out,
+              double *likelihood_out) {
+    if (!ctx) return set_err(nullptr, TD_ERR_ARG, "td_misfit: ctx is NULL");
+    if (n < 0 || n > 0x7fffffff || (n > 0 && (!ptS || !tS || !allSig)))
+        return set_err(ctx, TD_ERR_ARG, "td_misfit: bad arrays");
+    if (n == 0) {
+        if (phi_out) *phi_out = 0.0;  // MCsub.jl:169 C = 0
+        if (likelihood_out) *likelihood_out = 0.0;
+        return TD_OK;
+    }
+    TD_HIP(ctx, hipSetDevice(ctx->device));
+    if (n > ctx->mf_cap) {
+        if (ctx->mf_dev) (void)hipFree(ctx->mf_dev);
+        if (ctx->mf_host) (void)hipHostFree(ctx->mf_host);
+        ctx->mf_dev = ctx->mf_host = nullptr;
+        ctx->mf_cap = 0;
+        ctx->mf_tS.clear();
+        ctx->mf_sig.clear();
+        TD_HIP(ctx, hipMalloc(&ctx->mf_dev, sizeof(double) * (4 * (size_t)n + 1)));
+        TD_HIP(ctx, hipHostMalloc(&ctx->mf_host, sizeof(double) * ((size_t)n + 1)));
+        ctx->mf_cap = n;
+    }
+    double *d_ptS = ctx->mf_dev, *d_tS = d_ptS + n, *d_sig = d_tS + n, *d_terms = d_sig + n, *d_phi = d_terms + n;
+    // tS / sigma of a sharded run are the same every call: copied only when they change
+    const bool same = (int64_t)ctx->mf_tS.size() == n &&
+                      std::memcmp(ctx->mf_tS.data(), tS, sizeof(double) * (size_t)n) == 0 &&
+                      std::memcmp(ctx->mf_sig.data(), allSig, sizeof(double) * (size_t)n) == 0;
+    if (!same) {
+        ctx->mf_tS.assign(tS, tS + n);
+        ctx->mf_sig.assign(allSig, allSig + n);
+        ctx->mf_likelihood = likelihood_constant(allSig, n);
+        TD_HIP(ctx, hipMemcpyAsync(d_tS, tS, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+        TD_HIP(ctx, hipMemcpyAsync(d_sig, allSig, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    }
+    std::memcpy(ctx->mf_host, ptS, sizeof(double) * (size_t)n);
+    TD_HIP(ctx, hipMemcpyAsync(d_ptS, ctx->mf_host, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    hipError_t e = launch_chi2(d_ptS, d_tS, d_sig, (int)n, d_terms, d_phi, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->mf_host + n, d_phi, sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_err(ctx, e, "td_misfit");
+    if (phi_out) *phi_out = ctx->mf_host[n];
+    if (likelihood_out) *likelihood_out = ctx->mf_likelihood;  // MCsub.jl:179-182
     return TD_OK;
 }
 

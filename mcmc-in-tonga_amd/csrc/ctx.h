@@ -63,6 +63,12 @@ struct td_ctx {
     void *h_chain_desc = nullptr;       // pinned staging of the same
     tdstar::td_shadow *shadow = nullptr;  // td_evaluate's incremental path (incremental.cpp)
     int incremental = 2;                // 0 full evaluates; 1 one launch per call; 2 a resident server (tdt_set_incremental)
+    // td_misfit: device copies of the last (tS, sig) given and a pinned [ptS | phi] staging area
+    double *mf_dev = nullptr;           // [ptS n | tS n | sig n | terms n | phi 1]
+    double *mf_host = nullptr;          // pinned [ptS n | phi 1]
+    int64_t mf_cap = 0;
+    std::vector<double> mf_tS, mf_sig;  // what mf_dev holds
+    double mf_likelihood = 0.0;
     std::string err;
 };
 

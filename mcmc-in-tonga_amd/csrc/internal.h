@@ -161,6 +161,12 @@ hipError_t launch_nearest_grid(const double *qx, const double *qy, const double 
                                double *best_d, double *zeta0, hipStream_t s, Timer *tm = nullptr,
                                const double *stage = nullptr);
 
+// chi^2 of a given ptS (MCsub.jl:169-172, sequential in k, exact): the fused
+// one-workgroup scan up to 2048 rays, the block-wide scan beyond.  terms: n
+// doubles of scratch; phi: one double (device).
+hipError_t launch_chi2(const double *ptS, const double *tS, const double *sig, int n, double *terms, double *phi,
+                       hipStream_t s);
+
 // Testing: the block-wide exact sequential sum (exact_sum.h) on device buffers.
 hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fallbacks);
 hipError_t test_wave_delta_sum(const double *term, const double *old, const int *chg, int cnt, double C0,

@@ -535,6 +535,12 @@ hipError_t test_chi2(const double *ptS, const double *tS, const double *sig, int
     return hipGetLastError();
 }
 
+hipError_t launch_chi2(const double *ptS, const double *tS, const double *sig, int n, double *terms, double *phi,
+                       hipStream_t s) {
+    if (n <= 0) return hipMemsetAsync(phi, 0, sizeof(double), s);  // MCsub.jl:169 C = 0
+    return test_chi2(ptS, tS, sig, n, n <= kChi2Lds ? 0 : 1, terms, phi, s);
+}
+
 hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast) {
     hipLaunchKernelGGL(k_test_exact_sum, dim3(1), dim3(kChi2Threads), 0, nullptr, term, cnt, C0, prefix, C_end, fast);
     return hipGetLastError();

@@ -64,6 +64,16 @@ class TdContext:
         check(lib().td_get_info(self.h, ctypes.byref(info)), self.h)
         self.likelihood_const = float(info.likelihood)
 
+    def misfit(self, ptS, tS, allSig):
+        """(phi, likelihood) of a given ptS (MCsub.jl:169-182) on this device:
+        the reduction step of a ray-sharded evaluate (td_misfit)."""
+        p, t, s = f64(ptS), f64(tS), f64(allSig)
+        if not (len(p) == len(t) == len(s)):
+            raise ValueError("ptS, tS and allSig must have the same length")
+        phi, lk = ctypes.c_double(), ctypes.c_double()
+        check(lib().td_misfit(self.h, len(p), ptr(p), ptr(t), ptr(s), ctypes.byref(phi), ctypes.byref(lk)), self.h)
+        return phi.value, lk.value
+
     NN_AUTO, NN_BRUTE, NN_GRID, NN_BRUTE_SPLIT = 0, 1, 2, 3
 
     def set_nn_method(self, method):

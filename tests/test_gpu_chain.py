@@ -214,19 +214,21 @@ def test_bench_config_takes_lds_layout(tt, ds, ctx):
     ch.close()
 
 
-def test_stress_geometry_chain_follows_host_engine(tt):
+@pytest.mark.parametrize("ncells,rounds,seed", [(2000, 4, 51), (20000, 2, 5)])
+def test_stress_geometry_chain_follows_host_engine(tt, ncells, rounds, seed):
     """10k synthetic rays (the stress geometry): the HBM layout with super-tiles
     in LDS and the chi^2 event walk, bit for bit the host engine over a few
-    hundred proposals (accepted ones commit the walk's segments and re-mark)."""
+    hundred proposals (accepted ones commit the walk's segments and re-mark);
+    at 2000 cells and at config 5's full 20k cells (seed 5)."""
     ds = tt.synthetic_rays(10000, seed=5)
     ctx = tt.TdContext.from_datastruct(ds)
-    prm = tt.define_TDstructrure().replace(max_cells=3000)
-    model = tt.random_model(2000, 51)
-    dev = make(tt, ctx, prm, model, 51, tt.TD_ENGINE_DEVICE)
+    prm = tt.define_TDstructrure().replace(max_cells=int(ncells * 1.5))
+    model = tt.random_model(ncells, seed)
+    dev = make(tt, ctx, prm, model, seed, tt.TD_ENGINE_DEVICE)
     small, big, sup, layout = lds_plan(tt, dev)
     assert layout == 0 and sup == 1, (small, big, sup)
-    host = make(tt, ctx, prm, model, 51, tt.TD_ENGINE_HOST)
-    for _ in range(4):
+    host = make(tt, ctx, prm, model, seed, tt.TD_ENGINE_HOST)
+    for _ in range(rounds):
         dev.run(75)
         host.run(75)
         assert dev.stats()["phi"] == host.stats()["phi"]

@@ -67,3 +67,12 @@ def test_evaluate_phi_is_chi2_of_its_ptS(tt, kat, kat_ctx, orc):
         ptS, phi, _, _ = kat_ctx.evaluate(m.cells())
         assert chi2(tt, kat_ctx, ptS, 0)[0] == phi
         assert orc.chi2(ptS, kat["tS"], np.full(len(ptS), 0.2)) == phi
+
+
+def test_td_misfit_reproduces_model_jld(tt, kat, kat_ctx):
+    """td_misfit (the public chi^2 of a given ptS: the reduction of a ray-sharded
+    evaluate) returns the recorded phi and likelihood for all 100 records."""
+    sig = np.full(len(kat["tS"]), 0.2)
+    for k in range(len(kat["phi"])):
+        phi, lk = kat_ctx.misfit(kat["ptS"][k], kat["tS"], sig)
+        assert phi == kat["phi"][k] and lk == LIKELIHOOD_KAT, k
