@@ -24,6 +24,10 @@ def main():
     prm = tt.define_TDstructrure().replace(max_cells=10000)
     model = tt.random_model(5000, 3)
     chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=50000 + j, chain=10000 + j), model) for j in range(C)]
+    lds_mode = int(os.environ.get("TD_LDS_MODE", "0"))  # 1: the rays-in-HBM layout (testing)
+    if lds_mode:
+        for c in chains:
+            assert tt.lib().tdt_chain_set_lds_mode(c.h, lds_mode) == 0
     tt.run_batch(chains, iters)
     L = tt.lib()
     outs0 = []
