@@ -13,7 +13,11 @@
 //                strictly closer than every face of the block
 //                (grid_block_lb), i.e. than every cell outside, and no bucket
 //                of the block overflowed -- else the 5x5x5 block, else (rare)
-//                the same 32 lanes scan every cell.
+//                the same 32 lanes scan every cell;
+//   k_nn_grid4   the same search with 4 lanes per point (7 buckets each), for
+//                large point sets (>= 65536: the stress geometry, 254 -> 172 us
+//                at 584k points x 20k cells); the half-wave form keeps the
+//                small sets, where more waves and a wider fallback win.
 // Two launches per search: the bucket counts come in two sets used by
 // alternate searches, and each search's k_nn_grid zeroes the other set for
 // the next one (no memset, no third kernel).
@@ -23,6 +27,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "internal.h"
 #include "wave_ops.h"
@@ -156,6 +161,132 @@ __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, 
     }
 }
 
+
+// lexicographic min of (d, i) over each quad of lanes (4 lanes per point), to every lane of the quad
+__device__ __forceinline__ void quad_lexmin(double &d, int &i) {
+    constexpr unsigned long long I = ~0ull;
+    unsigned long long k = (unsigned long long)__double_as_longlong(d);
+    k = umin64(k, dpp_u64<0xB1, 0xf>(k, I));  // quad_perm [1,0,3,2]
+    k = umin64(k, dpp_u64<0x4E, 0xf>(k, I));  // quad_perm [2,3,0,1]
+    const bool at = (unsigned long long)__double_as_longlong(d) == k;
+    unsigned long long r = at ? (unsigned long long)(unsigned)i : I;
+    r = umin64(r, dpp_u64<0xB1, 0xf>(r, I));
+    r = umin64(r, dpp_u64<0x4E, 0xf>(r, I));
+    d = __longlong_as_double((long long)k);
+    i = r == I ? INT_MAX : (int)r;
+}
+
+// lexicographic min of (d, i) over the wave, to every lane
+__device__ __forceinline__ void wave_lexmin(double &d, int &i) {
+    const unsigned long long kd = wave_min_u64((unsigned long long)__double_as_longlong(d));
+    const bool at = (unsigned long long)__double_as_longlong(d) == kd;
+    const unsigned long long ki = wave_min_u64(at ? (unsigned long long)(unsigned)i : ~0ull);
+    d = __longlong_as_double((long long)kd);
+    i = ki == ~0ull ? INT_MAX : (int)ki;
+}
+
+// k_nn_grid with FOUR lanes per point (16 points per wave), for large point
+// sets (the stress geometry: the half-wave form spends ~200 wave-instructions
+// per point on reductions and the proof, these ~4x fewer).  Lane s of a quad
+// takes the buckets s, s + 4, ... of the 3x3x3 block (6 or 7): their counts
+// and first entries in one round of loads, then entry k of every bucket
+// holding more than k, one round each; then the quad's minimum.  A point the
+// block does not prove (rare) is finished by the whole wave, one point at a
+// time: the 5x5x5 block (two buckets per lane), else every cell.
+constexpr int kGridLpp = 4;
+constexpr int64_t kGridQuadMinPts = 65536;  // below: the half-wave kernel (more waves, shorter chains)
+__global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx, const double *__restrict__ qy,
+                                                  const double *__restrict__ qz, int npts, int ys, int zs, CellGrid G,
+                                                  const int *__restrict__ count, const BucketEntry *__restrict__ ent,
+                                                  const double *__restrict__ cells, int stride, int ncells,
+                                                  int *__restrict__ best_i, double *__restrict__ best_d,
+                                                  double *__restrict__ zeta0, int *__restrict__ other_count,
+                                                  int other_nb) {
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < other_nb; b += gridDim.x * blockDim.x) other_count[b] = 0;
+    const int lane = threadIdx.x & 63, sub = threadIdx.x & (kGridLpp - 1);
+    const int p = (blockIdx.x * blockDim.x + threadIdx.x) / kGridLpp;  // whole quads stay for the DPP
+    const int pc = min(p, npts - 1);
+    const double x = qx[pc], y = qy[(long)pc * ys], z = qz[(long)pc * zs];
+    const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
+              bk = grid_axis(z, G.z0, G.iz, G.gz);
+    constexpr int kMine = (27 + kGridLpp - 1) / kGridLpp;
+    int bb[kMine], cnt[kMine];
+    BucketEntry e[kMine];
+    bool over = false;
+    int most = 0;
+#pragma unroll
+    for (int u = 0; u < kMine; ++u) {  // counts and first entries: one round of loads
+        const int t = sub + u * kGridLpp;
+        const int ii = bi + t % 3 - 1, jj = bj + (t / 3) % 3 - 1, kk = bk + t / 9 - 1;
+        const bool inb = t < 27 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
+        bb[u] = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
+        cnt[u] = inb ? count[bb[u]] : 0;
+        e[u] = ent[(long)bb[u] * kGridCap];
+    }
+    double bd = kSentinel;
+    int bx = INT_MAX;
+#pragma unroll
+    for (int u = 0; u < kMine; ++u) {
+        over = over || cnt[u] > kGridCap;
+        cnt[u] = min(cnt[u], kGridCap);
+        most = max(most, cnt[u]);
+        if (cnt[u] > 0) take(dist2_q(e[u].x, e[u].y, e[u].z, x, y, z), e[u].slot, bd, bx);
+    }
+    for (int k = 1; k < most; ++k) {  // entry k of each of my buckets: one round of loads
+#pragma unroll
+        for (int u = 0; u < kMine; ++u)
+            if (k < cnt[u]) e[u] = ent[(long)bb[u] * kGridCap + k];
+#pragma unroll
+        for (int u = 0; u < kMine; ++u)
+            if (k < cnt[u]) take(dist2_q(e[u].x, e[u].y, e[u].z, x, y, z), e[u].slot, bd, bx);
+    }
+    quad_lexmin(bd, bx);
+    const int qsh = lane & ~(kGridLpp - 1);  // first lane of my quad
+    const bool any_over = ((__ballot(over) >> qsh) & 0xfull) != 0ull;
+    const bool proven = p >= npts || (!any_over && bd < grid_block_lb(G, x, y, z, 1));
+    // points the block does not prove: the whole wave, one at a time
+    unsigned long long need = __ballot(!proven && sub == 0);
+    while (need) {
+        const int src = __builtin_ctzll(need);
+        need &= need - 1;
+        const double px = readlane_f64(x, src), py = readlane_f64(y, src), pz = readlane_f64(z, src);
+        const int ci = __builtin_amdgcn_readlane(bi, src), cj = __builtin_amdgcn_readlane(bj, src),
+                  ck = __builtin_amdgcn_readlane(bk, src);
+        double d2 = kSentinel;
+        int i2 = INT_MAX;
+        bool over2 = false;
+        for (int t = lane; t < 125; t += 64) {  // the 5x5x5 block
+            const int ii = ci + t % 5 - 2, jj = cj + (t / 5) % 5 - 2, kk = ck + t / 25 - 2;
+            if (ii < 0 || ii >= G.gx || jj < 0 || jj >= G.gy || kk < 0 || kk >= G.gz) continue;
+            const int b = (kk * G.gy + jj) * G.gx + ii;
+            const int c = count[b];
+            over2 = over2 || c > kGridCap;
+            for (int k = 0; k < min(c, kGridCap); ++k) {
+                const BucketEntry f = ent[(long)b * kGridCap + k];
+                take(dist2_q(f.x, f.y, f.z, px, py, pz), f.slot, d2, i2);
+            }
+        }
+        wave_lexmin(d2, i2);
+        if (__ballot(over2) != 0ull || !(d2 < grid_block_lb(G, px, py, pz, 2))) {  // rare: every cell
+            d2 = kSentinel;
+            i2 = INT_MAX;
+            for (int j = lane; j < ncells; j += 64)
+                take(dist2_q(cells[j], cells[stride + j], cells[2 * (long)stride + j], px, py, pz), j, d2, i2);
+            wave_lexmin(d2, i2);
+        }
+        if (qsh == src) {
+            bd = d2;
+            bx = i2;
+        }
+    }
+    if (sub == 0 && p < npts) {
+        const bool found = bd < kSentinel;
+        best_i[p] = found ? bx : -1;
+        if (best_d) best_d[p] = bd;
+        if (zeta0) zeta0[p] = found ? cells[3 * (long)stride + bx] : 0.0;  // MCsub.jl:249
+    }
+}
+
 }  // namespace
 
 hipError_t launch_nearest_grid(const double *qx, const double *qy, const double *qz, int64_t npts,
@@ -191,9 +322,19 @@ hipError_t launch_nearest_grid(const double *qx, const double *qy, const double 
                        (int)stride, (int)ncells, G, count, work.g_ent);
     if (tm) tm->end("nn_grid_build", t0, s);
     hipEvent_t t1 = tm ? tm->begin(s) : nullptr;
-    hipLaunchKernelGGL(k_nn_grid, dim3((unsigned)((npts + 7) / 8)), dim3(256), 0, s, qx, qy, qz, (int)npts,
-                       (int)qy_stride, (int)qz_stride, G, count, work.g_ent, cells, (int)stride, (int)ncells,
-                       best_i, best_d, zeta0, other, (int)work.g_used[par ^ 1]);
+    static const int grid_form = [] {  // diagnostic override: 1 half-wave, 4 quad
+        const char *v = std::getenv("TD_NN_GRID_FORM");
+        return v ? std::atoi(v) : 0;
+    }();
+    const bool quad = grid_form ? grid_form == 4 : npts >= kGridQuadMinPts;
+    if (!quad)
+        hipLaunchKernelGGL(k_nn_grid, dim3((unsigned)((npts + 7) / 8)), dim3(256), 0, s, qx, qy, qz, (int)npts,
+                           (int)qy_stride, (int)qz_stride, G, count, work.g_ent, cells, (int)stride, (int)ncells,
+                           best_i, best_d, zeta0, other, (int)work.g_used[par ^ 1]);
+    else
+        hipLaunchKernelGGL(k_nn_grid4, dim3((unsigned)((npts * kGridLpp + 255) / 256)), dim3(256), 0, s, qx, qy, qz,
+                           (int)npts, (int)qy_stride, (int)qz_stride, G, count, work.g_ent, cells, (int)stride,
+                           (int)ncells, best_i, best_d, zeta0, other, (int)work.g_used[par ^ 1]);
     if (tm) tm->end("nn_grid", t1, s);
     e = hipGetLastError();
     if (e == hipSuccess) {
