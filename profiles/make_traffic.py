@@ -19,6 +19,7 @@ ROWS = {  # traffic.json key -> (run, kernel name)
     "k_nn_tile/config3": ("single", "k_nn_tile<2>"),
     "k_nn_grid/config3": ("single", "k_nn_grid"),
     "k_chain_run/stress": ("stress", "k_chain_run<false>"),
+    "k_nn_grid4/stress": ("stress", "k_nn_grid4"),
 }
 
 
