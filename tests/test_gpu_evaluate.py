@@ -294,3 +294,38 @@ def test_tile_brute_force_plans(tt, orc, ctx, npts):
             assert np.array_equal(near, ref_ids), (m, nc, np.flatnonzero(near != ref_ids)[:5])
             assert np.array_equal(zr, ref), (m, nc)
     ctx.set_nn_method(ctx.NN_AUTO)
+
+
+def test_grid_large_query_sets(tt, orc, ctx):
+    """Query sets of >= 65,536 points take the 4-lanes-per-point grid kernel
+    (k_nn_grid4); it and its fallbacks (points outside the cells' box,
+    unproven blocks, overfull buckets) against the oracle: lattice cells with
+    queries on bucket faces,
+    a tight cluster (every point falls back to the wave-wide passes), NaN
+    cells, duplicated cells (ties across buckets), cells far from the
+    queries."""
+    rng = np.random.default_rng(21)
+    xmin, xmax, ymin, ymax, zmin, zmax = tt.box()
+    n = 70000
+    X = np.concatenate([rng.uniform(xmin, xmax, n - 2048), np.arange(0, 1024, 1.0) * 1.0, rng.uniform(-3e3, 3e3, 1024)])
+    Y = np.concatenate([rng.uniform(ymin, ymax, n - 2048), np.full(1024, 50.0), rng.uniform(-3e3, 3e3, 1024)])
+    Z = np.concatenate([rng.uniform(zmin, zmax, n - 2048), np.arange(0, 1024, 1.0) % 650, rng.uniform(-1e3, 1e3, 1024)])
+    ix, iy, iz = np.meshgrid(np.arange(0, 1000, 50.0), np.arange(-250, 400, 50.0), np.arange(0, 650, 50.0),
+                             indexing="ij")
+    lattice = (ix.ravel(), iy.ravel(), iz.ravel(), 3.0 + (ix.ravel() % 7))
+    m = tt.random_model(3000, 23)
+    x, y, z, zeta = (a.copy() for a in m.cells())
+    x[::50] = np.nan
+    k = 600
+    x[-k:], y[-k:], z[-k:] = x[:k], y[:k], z[:k]  # duplicates: the lower index must win
+    zeta[-k:] = zeta[:k] + 1.0
+    clus = (400 + rng.uniform(0, 1, 500), 100 + rng.uniform(0, 1, 500), 300 + rng.uniform(0, 1, 500),
+            rng.uniform(1, 49, 500))
+    far = (rng.uniform(5e4, 6e4, 500), rng.uniform(5e4, 6e4, 500), rng.uniform(0, 10, 500), rng.uniform(1, 49, 500))
+    for cells in (lattice, (x, y, z, zeta), clus, far):
+        ref, ref_ids = orc.interpolation(cells, X, Y, Z)
+        ctx.set_nn_method(ctx.NN_GRID)
+        zr, near = ctx.interpolate(cells, X, Y, Z, want_nearest=True)
+        ctx.set_nn_method(ctx.NN_AUTO)
+        assert np.array_equal(near, ref_ids), np.flatnonzero(near != ref_ids)[:5]
+        assert np.array_equal(zr, ref)
