@@ -679,7 +679,10 @@ struct CopySeg {
     }
 };
 
-template <bool SMALL>
+// SCRIPT: host-given proposals (td_evaluate's incremental path: scripted
+// steps, the resident server); a free-running chain's instance has none of
+// that code on its path.
+template <bool SMALL, bool SCRIPT>
 __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters,
                                                              ScriptArgs sa) {
     constexpr bool WALK = !SMALL || kSmallWalk;  // chi^2 by the event walk
@@ -699,8 +702,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const int n = d.n, NT = d.ntiles;
     const bool prof_on = d.profile != 0;
     const long long t_start = prof_on ? clock64() : 0;  // diagnostic: launch preamble / epilogue (prof[76..79])
-    Mailbox *const mb = sa.mb;  // server mode: resident, steps from the mailbox (iters ignored)
-    const int nscript = mb ? 1 : sa.n;  // > 0: host-given proposals (td_evaluate), iters == nscript
+    Mailbox *const mb = SCRIPT ? sa.mb : nullptr;  // server mode: resident, steps from the mailbox (iters ignored)
+    const int nscript = SCRIPT ? (mb ? 1 : sa.n) : 0;  // > 0: host-given proposals (td_evaluate), iters == nscript
 
     // ---- views: LDS copies of the tile / ray / order arrays when they fit ----
     Views v;
@@ -1638,13 +1641,30 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
         big = std::max(big, lds_plan(d.ntiles, d.n, d.cap, false).total);
         force_hbm = force_hbm || d.lds_mode == 1;
     }
+    const bool scripted = sa.n > 0 || sa.mb != nullptr;
+    static bool attr_set = false;  // dynamic LDS above 64 KB needs the attribute (once per kernel)
+    if (!attr_set) {
+        for (const void *k : {(const void *)k_chain_run<true, false>, (const void *)k_chain_run<true, true>,
+                              (const void *)k_chain_run<false, false>, (const void *)k_chain_run<false, true>}) {
+            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
+            if (e != hipSuccess) return e;
+        }
+        attr_set = true;
+    }
     if (small <= kLdsBudget && !force_hbm) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_chain_run<true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)small);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_chain_run<true>, dim3(grid), dim3(kChainThreads), small, s, dev, (long long)iters, sa);
+        if (scripted)
+            hipLaunchKernelGGL((k_chain_run<true, true>), dim3(grid), dim3(kChainThreads), small, s, dev,
+                               (long long)iters, sa);
+        else
+            hipLaunchKernelGGL((k_chain_run<true, false>), dim3(grid), dim3(kChainThreads), small, s, dev,
+                               (long long)iters, sa);
     } else {
-        hipLaunchKernelGGL(k_chain_run<false>, dim3(grid), dim3(kChainThreads), big, s, dev, (long long)iters, sa);
+        if (scripted)
+            hipLaunchKernelGGL((k_chain_run<false, true>), dim3(grid), dim3(kChainThreads), big, s, dev,
+                               (long long)iters, sa);
+        else
+            hipLaunchKernelGGL((k_chain_run<false, false>), dim3(grid), dim3(kChainThreads), big, s, dev,
+                               (long long)iters, sa);
     }
     return hipGetLastError();
 }
