@@ -1279,15 +1279,21 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 __syncthreads();
                 if (tid == 0) acc_r = sh.accept != 0;
             }
+            // the changed points' global records (two dependent L2 round trips) and the
+            // deleteat! shift go to waves 1.., so wave 0 goes straight to its scalars and
+            // the next proposal (kW threads, index w = tid - 64)
+            constexpr int kW = kChainThreads - 64;
+            const int w = tid - 64;
             if (sh.accept) {
                 const int nt = sh.n_tiles, k0 = sh.k0;
-                for (int c = tid; c < nc; c += kChainThreads) {
-                    const int q = d.changed[c];
-                    d.best_s[q] = d.cand_s[q];
-                    d.best_d[q] = d.cand_d[q];
-                    d.zeta0[q] = d.cand_z[q];
-                    d.cand_flag[q] = 0;
-                }
+                if (wv != 0)
+                    for (int c = w; c < nc; c += kW) {
+                        const int q = d.changed[c];
+                        d.best_s[q] = d.cand_s[q];
+                        d.best_d[q] = d.cand_d[q];
+                        d.zeta0[q] = d.cand_z[q];
+                        d.cand_flag[q] = 0;
+                    }
                 if (fwd && action != tdchain::kChange) {
                     for (int i = tid; i < nt; i += kChainThreads) v.tmaxd[v.tile_rec(i).x] = v.ctm[i];
                     pend_sup = super_on;  // their super-tiles' maxima: at the top of the next iteration
@@ -1303,12 +1309,22 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     pend_r = true;  // written at the top of the next iteration
                     if (wv == 1) delta_remark(v.term, v.prefix, v.cprefix, n, sh.dseg, smask, lane);
                 }
-                if (action == tdchain::kDeath)  // deleteat!: positions after the killed one shift down
-                    for (int j = (int)pp.index + 1 + tid; j < ncells; j += kChainThreads) {
-                        const int s = d.order_tmp[j];
-                        v.ord[j - 1] = s;
-                        d.rank[s] = j - 1;
+                if (action == tdchain::kDeath && wv != 0) {  // deleteat!: positions after the killed one shift down
+                    constexpr int U = 4;                         // U loads in flight per thread
+                    for (int j0 = (int)pp.index + 1 + w; j0 < ncells; j0 += U * kW) {
+                        int sl[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) sl[u] = d.order_tmp[min(j0 + u * kW, ncells - 1)];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int j = j0 + u * kW;
+                            if (j < ncells) {
+                                v.ord[j - 1] = sl[u];
+                                d.rank[sl[u]] = j - 1;
+                            }
+                        }
                     }
+                }
                 if (tid == kChainThreads - 64 && sh.g_op) grid_apply(d, sh);
                 if (tid == 0) {
                     const int sk = slot_k;
@@ -1349,7 +1365,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.phi = phi_r;
                 }
             } else {  // rejected: flags down, the changed rays get their old chi^2 terms back
-                for (int c = tid; c < nc; c += kChainThreads) d.cand_flag[d.changed[c]] = 0;
+                if (wv != 0)
+                    for (int c = w; c < nc; c += kW) d.cand_flag[d.changed[c]] = 0;
                 for (int rr = tid; rr < nr; rr += kChainThreads) {
                     const int r = v.ray_at(rr);
                     v.term[r] = v.cterm[r];
