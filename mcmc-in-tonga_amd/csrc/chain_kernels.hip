@@ -48,6 +48,8 @@ using tdchain::Proposal;
 constexpr int kWaves = kChainThreads / 64;
 static_assert(kTilePts == 16, "a tile is one 16-lane DPP row (row_max_u64)");
 constexpr int kOrphanLds = 256; // orphan records kept in LDS (more: read back from HBM)
+constexpr int kPre = 64 / kTilePts;  // LDS layout: hit tiles per wave whose points phase B preloads
+static_assert(kPre == 4, "the preload slots are four registers");
 constexpr int kListLds = 1024;  // rays in HBM: hit tiles / changed rays / hit super-tiles kept in LDS
 // The LDS layout could sum chi^2 with the event walk too; its tails are ~60 terms and the
 // one-wave binade scan with the early-rejection bound is faster there (measured: the walk
@@ -288,7 +290,7 @@ struct Views {
     // hit tile i: {tile, start << 5 | count, ray}
     __device__ __forceinline__ int4 tile_rec(int i) const {
         if (i < hrec_cap) return hrec[i];
-        const int t = thit[i];
+        const int t = thit[i] & 0x7fffffff;  // LDS layout: the high bit marks a tile preloaded in phase B
         return int4{t, tstart[t], tray[t], 0};
     }
 };
@@ -903,6 +905,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         const double zeta_killed = cur.zeta_killed;
         double czeta = 0.0, zetanew_death = 0.0;
         STAMP(0);
+        // LDS layout: the points of the first kPre hit tiles a wave finds are loaded in
+        // phase B (their global round trip overlaps the B barrier and the birth/death
+        // query) and judged in phase C
+        bool pre_on = false;
+        int pre_q = 0, pre_ray = 0, pre_s = 0;
+        double pre_bd = 0.0, pre_x = 0.0, pre_y = 0.0, pre_z = 0.0;
         if (p.active) {
             // ============ phase B: tile pass || birth/death Interpolation ============
             // (a scripted step brings its own values: no Interpolation query)
@@ -965,6 +973,61 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                                     if (k < v.hrec_cap) v.hrec[k] = rec[u];
                                 }
                         }
+                } else if (SMALL) {
+                    if (tid < nthr) {  // wave-uniform
+                        int npre = 0;  // preload slots this wave has taken (wave-uniform)
+                        int pt[kPre] = {0, 0, 0, 0};  // their tiles (wave-uniform: from the ballots, no LDS)
+                        for (int b0 = wv * 64; b0 < NT; b0 += TU * nthr) {  // the same trip count in every lane
+                            const int t0 = b0 + lane;
+                            bool hit[TU];
+#pragma unroll
+                            for (int u = 0; u < TU; ++u) {
+                                const int t = min(t0 + u * nthr, NT - 1);  // clamped: loads stay unconditional
+                                const float thr = tile_thr(v.tmaxd[t]);
+                                const bool h0 = tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr);
+                                const bool h1 = tile_may_hit(v.tlo, v.thi, NT, t, tq1, thr);
+                                hit[u] = t0 + u * nthr < NT && ((q0 && h0) || (q1 && h1));
+                            }
+#pragma unroll
+                            for (int u = 0; u < TU; ++u) {
+                                const unsigned long long m = __ballot(hit[u]);
+                                if (m == 0ull) continue;
+                                const int first = __builtin_ctzll(m), cnt = __popcll(m);
+                                const int rank = __popcll(m & ((1ull << lane) - 1ull));
+                                int base = 0;
+                                if (lane == first) base = atomicAdd(&sh.n_tiles, cnt);  // one atomic per wave
+                                base = __builtin_amdgcn_readlane(base, first);
+                                if (hit[u]) {
+                                    const int t = t0 + u * nthr, slot = npre + rank;
+                                    v.thit[base + rank] = slot < kPre ? (t | INT_MIN) : t;
+                                }
+                                for (unsigned long long mm = m; mm && npre < kPre; mm &= mm - 1ull) {
+                                    const int t = b0 + __builtin_ctzll(mm) + u * nthr;
+#pragma unroll
+                                    for (int k = 0; k < kPre; ++k) pt[k] = k == npre ? t : pt[k];
+                                    ++npre;
+                                }
+                            }
+                        }
+                        if (npre > 0) {
+                            if (lane < kTilePts * npre) {
+                                const int g = lane / kTilePts;
+                                const int t = g == 0 ? pt[0] : g == 1 ? pt[1] : g == 2 ? pt[2] : pt[3];
+                                const int sc = v.tstart[t];
+                                if (lane % kTilePts < (sc & 31)) {
+                                    const int q = (sc >> 5) + lane % kTilePts;
+                                    pre_on = true;
+                                    pre_q = q;
+                                    pre_ray = v.tray[t];
+                                    pre_s = d.best_s[q];  // independent loads: one round trip
+                                    pre_bd = d.best_d[q];
+                                    pre_x = d.px[q];
+                                    pre_y = d.py[q];
+                                    pre_z = d.pz[q];
+                                }
+                            }
+                        }
+                    }
                 } else if (tid < nthr)
                     for (int t0 = tid; t0 < NT; t0 += TU * nthr) {
                         bool hit[TU];
@@ -1030,8 +1093,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     }
                 };
                 if constexpr (SMALL) {
+                    if (pre_on) {  // loaded in phase B
+                        ++seen;
+                        point(pre_q, pre_ray, pre_s, pre_bd, pre_x, pre_y, pre_z);
+                    }
                     for (int item = tid; item < nt * kTilePts; item += kChainThreads) {
                         const int t = v.thit[item / kTilePts];
+                        if (t < 0) continue;  // preloaded
                         const int sc = v.tstart[t];  // start << 5 | count
                         if (item % kTilePts >= (sc & 31)) continue;
                         const int q = (sc >> 5) + item % kTilePts;
