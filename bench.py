@@ -435,7 +435,7 @@ def stress(tt, chain_iters=2000):
     ctx.timing(enable=False)
     res["chain"] = {"proposals_per_s": round(chain_iters / el, 1), "iters": chain_iters,
                     "layout": "hbm (tiles, rays, order do not fit in LDS)",
-                    "roofline": chain_roofline("k_chain_run<false>", model_bytes(int(ctx.P), int(ctx.n), 20000),
+                    "roofline": chain_roofline("k_chain_run<false, false> (rays in HBM)", model_bytes(int(ctx.P), int(ctx.n), 20000),
                                                chain_iters, kms / 1e3 / max(launches, 1), ch.stats()["bytes"] - b0,
                                                "k_chain_run/stress", chain_iters == 2000)}
     ch.close()
