@@ -873,6 +873,24 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     long long it_done = 0;                 // iterations run (server mode: until QUIT)
     for (long long it = 0; it < iters && !(mb && sh.srv_quit); ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
+        // rays in HBM: the previous accepted proposal's super-tile maxima (their first round of
+        // loads issued here, so it overlaps the partial sums' commit below)
+        int sup_n = 0, sup_S = 0, sup_par = 0;
+        bool sup_all = false;
+        unsigned long long sup_mk = 0ull;
+        if constexpr (!SMALL) {
+            if (pend_sup) {
+                sup_par = (int)((it - 1) & 1);
+                const int nsh = sh.n_super[sup_par];
+                sup_all = nsh > kListLds;  // the list overflowed: every super-tile
+                sup_n = sup_all ? NS : nsh;
+                if ((tid >> 4) < sup_n) {
+                    sup_S = sup_all ? (tid >> 4) : shit[sup_par * kListLds + (tid >> 4)];
+                    const int t = sup_S * kTilePts + (tid & 15);
+                    sup_mk = t < NT ? (unsigned long long)__double_as_longlong(d.tile_maxd[t]) : 0ull;
+                }
+            }
+        }
         if constexpr (WALK) {
             // the previous accepted proposal's partial sums (read again only in phase F,
             // after at least one barrier): off its critical path, before this one's tiles
@@ -881,10 +899,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         }
         if constexpr (!SMALL) {
             if (pend_sup) {  // its hit super-tiles: max of their tiles' new maxima (a tile row each)
-                const int par = (int)((it - 1) & 1), nsh = sh.n_super[par];
-                const bool all = nsh > kListLds;  // the list overflowed: every super-tile
-                for (int i = tid >> 4; i < (all ? NS : nsh); i += kChainThreads / kTilePts) {
-                    const int S = all ? i : shit[par * kListLds + i], t = S * kTilePts + (tid & 15);
+                if ((tid >> 4) < sup_n) {  // whole rows: the DPP row max
+                    const unsigned long long mk = row_max_u64(sup_mk);
+                    if ((tid & 15) == 15) smax[sup_S] = f32_up(__longlong_as_double((long long)mk));
+                }
+                for (int i = (tid >> 4) + kChainThreads / kTilePts; i < sup_n; i += kChainThreads / kTilePts) {
+                    const int S = sup_all ? i : shit[sup_par * kListLds + i], t = S * kTilePts + (tid & 15);
                     unsigned long long mk = t < NT ? (unsigned long long)__double_as_longlong(d.tile_maxd[t]) : 0ull;
                     mk = row_max_u64(mk);
                     if ((tid & 15) == 15) smax[S] = f32_up(__longlong_as_double((long long)mk));
@@ -1169,11 +1189,36 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // ================= phase E: t* of the rays that changed =================
                 const int nr = sh.n_rays;
                 const OverlayZeta oz{d.cand_flag, d.cand_z, d.zeta0};
-                for (int rr = wv; rr < nr; rr += kWaves) {
-                    const int r = v.ray_at(rr);
-                    const int s0 = v.ray_off[r];
-                    const int npr = v.ray_off[r + 1] - s0;
-                    const double tsr = v.tS[r], sgr = v.sig[r], old_term = v.term[r];  // with the offsets
+                // rays in HBM: a wave's rays' offsets, tS, sigma and old terms, one per lane,
+                // in one round of loads before its first sum (the 64 first; more: per ray)
+                int ra = 0, s0a = 0, e0a = 0;
+                double tsa = 0.0, sga = 0.0, ota = 0.0;
+                if (!SMALL && wv + kWaves * lane < nr && lane < 64) {
+                    ra = v.ray_at(wv + kWaves * lane);
+                    s0a = v.ray_off[ra];
+                    e0a = v.ray_off[ra + 1];
+                    tsa = v.tS[ra];
+                    sga = v.sig[ra];
+                    ota = v.term[ra];
+                }
+                for (int rr = wv, j = 0; rr < nr; rr += kWaves, ++j) {
+                    int r, s0, npr;
+                    double tsr, sgr, old_term;
+                    if (!SMALL && j < 64) {
+                        r = __builtin_amdgcn_readlane(ra, j);
+                        s0 = __builtin_amdgcn_readlane(s0a, j);
+                        npr = __builtin_amdgcn_readlane(e0a, j) - s0;
+                        tsr = readlane_f64(tsa, j);
+                        sgr = readlane_f64(sga, j);
+                        old_term = readlane_f64(ota, j);
+                    } else {
+                        r = v.ray_at(rr);
+                        s0 = v.ray_off[r];
+                        npr = v.ray_off[r + 1] - s0;
+                        tsr = v.tS[r];  // with the offsets
+                        sgr = v.sig[r];
+                        old_term = v.term[r];
+                    }
                     const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
                     if (lane == 0) {
                         v.cptS[r] = val;
