@@ -153,6 +153,29 @@ int64_t common_prefix(const double *const in[4], const View &v, int64_t lim) {
     return lim;
 }
 
+// O(1) guess whether `in` (M cells) descends from Q = B + e rather than from B:
+// it holds e's mark where e left it (the appended cell at N, the cell after the
+// killed one at k, the new value or site at k).  Only an order for the two
+// classify scans (each reads the whole model): whichever base matches, the
+// model evaluated is `in`, exactly.
+bool looks_like_q(const double *const in[4], int64_t M, const Cells &B, const ScriptStep &e) {
+    const int64_t N = B.size(), k = e.index;
+    auto eq = [](double a, double b) { return std::memcmp(&a, &b, sizeof(double)) == 0; };
+    switch (e.action) {
+        case 1:  // birth: Q has N + 1 cells, the new one last
+            return M >= N + 1 && eq(in[0][N], e.x) && eq(in[1][N], e.y) && eq(in[2][N], e.z);
+        case 2:  // death of k: Q[k] = B[k + 1]
+            return k + 1 < N && k < M && !(eq(in[0][k], B.x[(size_t)k]) && eq(in[1][k], B.y[(size_t)k])) &&
+                   eq(in[0][k], B.x[(size_t)k + 1]) && eq(in[1][k], B.y[(size_t)k + 1]);
+        case 3:  // change of k
+            return k < M && eq(in[3][k], e.zeta);
+        case 4:  // move of k
+            return k < M && eq(in[0][k], e.x) && eq(in[1][k], e.y) && eq(in[2][k], e.z);
+        default:
+            return false;
+    }
+}
+
 // Is `in` (M cells) the model `base` plus one reference-shaped edit?  0:
 // identical, 1: one edit (in *e, decision unset), -1: neither.
 int classify(const double *const in[4], int64_t M, const View &base, ScriptStep *e) {
@@ -289,13 +312,23 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
     ScriptStep e2;
     ScriptStep steps[kMaxScript];
     int nsteps = 0, decision = 0;  // decision: the fate of the device's pending proposal
-    const int rb = classify(in, M, View(s->B, nullptr), &e2);
+    // an edit of Q when the O(1) probe says so (Julia accepted Q: ~57 % of calls), else of B;
+    // the other base only when the first scan fails (one model scan per call, mostly)
+    int rq = -2;  // -2: Q not tried yet
+    if (s->pending && looks_like_q(in, M, s->B, s->e)) {
+        rq = classify(in, M, View(s->B, &s->e), &e2);
+        if (rq == 0) return out(s->phiQ, s->ptSQ);
+    }
+    const int rb = rq == 1 ? -1 : classify(in, M, View(s->B, nullptr), &e2);
     if (rb == 0) return out(s->phiB, s->ptSB);
     if (rb == 1 && s->pending && std::memcmp(&e2, &s->e, sizeof e2) == 0) return out(s->phiQ, s->ptSQ);  // == Q again
     if (rb == 1) {
         s->pending = false;  // Q (if any) was rejected: undone (decision 0)
     } else if (s->pending) {
-        const int rq = classify(in, M, View(s->B, &s->e), &e2);
+        if (rq == -2 || rq == -1) {
+            if (rq == -1) return full();  // neither base
+            rq = classify(in, M, View(s->B, &s->e), &e2);
+        }
         if (rq < 0) return full();
         if (rq == 0) return out(s->phiQ, s->ptSQ);
         if (s->dev_pending) {
