@@ -39,6 +39,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
+# A latency floor for one chain proposal: the phases' dependent steps
+# priced with the primitives measured on the MI355X (tools/microbench.hip):
+# block barrier 350 cycles, dependent L2 hit 220, LDS round trip 90, FP64 add 30.
+LATENCY_FLOOR_MODEL = {
+    "B tile pass": (1, 0, 2, 0),       # (barriers, L2 trips, LDS trips, dependent FP64 ops)
+    "C points": (1, 1, 3, 8),
+    "D orphans (death, move: half)": (0.5, 1, 1.5, 6),
+    "E ray sums": (1, 1, 2, 10),
+    "F chi2 tail + decision": (1, 0, 2, 58 + 10),  # ~58-term tail added in order, 10 ops for alpha
+    "G commit + next proposal": (2, 0, 2, 0),
+}
+LATENCY_PRICES = (350.0, 220.0, 90.0, 30.0)
+CLOCK_GHZ = 2.4
+
+
+def latency_floor_us():
+    cyc = sum(sum(n * c for n, c in zip(v, LATENCY_PRICES)) for v in LATENCY_FLOOR_MODEL.values())
+    return cyc / (CLOCK_GHZ * 1e3)
 FP64_VALU_PEAK_TFLOPS = 78.6   # FP64 vector, FMA counted as 2 (spec)
 # the distance kernel may not use FMA (bit-exactness), so its roof is half that
 FP64_NOFMA_PEAK_TFLOPS = FP64_VALU_PEAK_TFLOPS / 2
@@ -245,6 +263,14 @@ def main():
                                    bytes_per_launch, "k_chain_run/single",
                                    C == 1 and ladder is None and N == 5000 and a.iters_per_step == 5000),
     }
+    if C == 1:  # the bound that applies to one chain: its chain of dependent steps
+        us = avg_s / max(a.iters_per_step, 1) * 1e6
+        fl = latency_floor_us()
+        out["roofline"]["latency_floor"] = {
+            "us_per_proposal": round(fl, 3), "achieved_us_per_proposal": round(us, 3), "frac": round(fl / us, 4),
+            "model": "sum over phases B-G of barriers x 350 + dependent L2 trips x 220 + LDS trips x 90 + "
+                     "dependent FP64 ops x 30 cycles at 2.4 GHz (microbench.hip prices; DESIGN.md 4.2): %s"
+                     % {k: v for k, v in LATENCY_FLOOR_MODEL.items()}}
     if ladder is not None:
         out["tempering"] = {"replicas": ladder.R, "temps": [round(t, 4) for t in ladder.temps],
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
