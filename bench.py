@@ -135,7 +135,7 @@ def parse():
     ap.add_argument("--tmax", type=float, default=8.0)
     ap.add_argument("--batch-chains", type=int, default=256,
                     help="size of the extra many-chains-per-GPU measurement on rank 0 (0 = skip)")
-    ap.add_argument("--batch-iters", type=int, default=1000)
+    ap.add_argument("--batch-iters", type=int, default=5000)
     ap.add_argument("--no-config4", dest="config4", action="store_false",
                     help="skip the config-4 block (8 tempered replicas x 2000 cells, swap every 10, one GPU)")
     ap.add_argument("--no-stress", action="store_true",
@@ -350,7 +350,7 @@ def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3):
     value = C * iters * steps / el
     avg_s = kms / 1e3 / max(launches, 1)
     roof = chain_roofline("k_chain_run (grid = %d chains)" % C, model_bytes(int(ctx.P), int(ctx.n), len(model.xCell)),
-                          C * iters, avg_s, nbytes / max(launches, 1), "k_chain_run/many256", C == 256 and iters == 1000)
+                          C * iters, avg_s, nbytes / max(launches, 1), "k_chain_run/many256", C == 256 and iters == 5000)
     roof["note"] = ("the full-evaluate byte model exceeds HBM peak here: the incremental kernel does not read what a "
                     "full evaluate reads (its working set stays in LDS / L2), see frac_measured_traffic")
     return {"chains": C, "proposals_per_s": round(value, 1), "per_chain_proposals_per_s": round(value / C, 1),

@@ -50,7 +50,11 @@ def main():
                       "proposals_per_s": n / el,
                       "cycles_per_iter_per_chain": {p: round(c / n, 1) for p, c in zip(PHASES, cyc)},
                       "total": round(cyc.sum() / n, 1),
-                      "F per wave": [round(tot[56 + w] / n, 1) for w in range(8)]}, indent=1))
+                      "F per wave": [round(tot[56 + w] / n, 1) for w in range(8)],
+                      # per launch, averaged over the chains: preamble (mirrors, terms, draws) and epilogue
+                      "preamble cycles per launch": round(tot[76] / max(tot[78], 1), 1),
+                      "epilogue cycles per launch": round(tot[77] / max(tot[78], 1), 1),
+                      "launches": int(tot[78] / C)}, indent=1))
 
 
 if __name__ == "__main__":

@@ -15,5 +15,5 @@ run() {  # name, bench args...
 }
 mkdir -p $OUT/single $OUT/many $OUT/stress
 run single --steps 3 --warmup 1 --no-cpu-baseline --batch-chains 0 --no-stress --no-dropin --no-config4 && \
-run many --steps 2 --warmup 1 --no-cpu-baseline --no-full-evaluate --no-dropin --no-config4 --no-stress --batch-chains 0 --chains-per-gpu 256 --iters-per-step 1000 && \
+run many --steps 2 --warmup 1 --no-cpu-baseline --no-full-evaluate --no-dropin --no-config4 --no-stress --batch-chains 0 --chains-per-gpu 256 --iters-per-step 5000 && \
 run stress --steps 1 --warmup 0 --iters-per-step 10 --no-cpu-baseline --no-full-evaluate --no-dropin --no-config4 --batch-chains 0
