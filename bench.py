@@ -288,7 +288,7 @@ def main():
         out["config4_tempering"] = tempering_config4(tt, ctx, ds)
     if rank == 0 and a.batch_chains > 0:
         out["many_chains"] = many_chains(tt, ctx, ds, prm, model, a.batch_chains, a.batch_iters)
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the host-core baseline: N = 1 only
         out["cpu_baseline"] = cpu_baseline(ds, model, a.cpu_seconds)
         if out["cpu_baseline"]["value"] > 0:
             out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
