@@ -1,4 +1,6 @@
-# A/B: the round-1 snapshot (variants/r01, git worktree of 93c8312) vs HEAD, single chain config 3, same box
+# A/B: the round-1 snapshot vs HEAD, single chain config 3, same box.  Needs the snapshot
+# built in-tree first: git worktree add -f variants/r01 93c8312 && make -C variants/r01/mcmc-in-tonga_amd/csrc
+# (variants/ is git-ignored, not gpurun-ignored: it travels to the box)
 set -e
 mkdir -p gpurun_out
 A="--steps 10 --warmup 2 --no-cpu-baseline --no-full-evaluate --no-stress --batch-chains 0"
