@@ -286,12 +286,20 @@ def main():
         out["stress"] = stress(tt)
     if rank == 0 and a.config4:
         out["config4_tempering"] = tempering_config4(tt, ctx, ds)
+    if rank == 0 and not a.no_full_evaluate:  # SURVEY 8f rows 2 and 4, measured beside their CPU restatements
+        out["posterior_maps"] = posterior_maps(tt, ctx, ds)
+        out["ingest_trilinear"] = ingest_trilinear(tt)
     if rank == 0 and a.batch_chains > 0:
         out["many_chains"] = many_chains(tt, ctx, ds, prm, model, a.batch_chains, a.batch_iters)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the host-core baseline: N = 1 only
-        out["cpu_baseline"] = cpu_baseline(ds, model, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(ds, model, a.cpu_seconds, tt if not a.no_full_evaluate else None)
         if out["cpu_baseline"]["value"] > 0:
             out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
+        aux = out["cpu_baseline"].get("aux", {})
+        for key, unit in (("posterior_maps", "ms_per_section"), ("ingest_trilinear", "ms")):
+            if key in aux and key in out and out[key][unit] > 0:
+                out[key]["cpu_baseline"] = aux[key]
+                out[key]["speedup_vs_cpu_baseline"] = round(aux[key][unit] / out[key][unit], 1)
     for c in chains:
         c.close()
     if rank == 0:
@@ -499,6 +507,62 @@ def stress_sharded(tt, ex, dist, coll_dev, device, reps=10):
     return res
 
 
+def posterior_inputs(tt, ds, nmodels=100, ncells=5000):
+    """plot_model_hist's workload (MCsub.jl:753-781): one xz section at the
+    reference's node grid (xVec x zVec, y = 100 km) over `nmodels` saved models
+    of `ncells` cells (synthetic, seeded)."""
+    models = [tt.random_model(ncells, 700 + k).cells() for k in range(nmodels)]
+    xv, zv = np.asarray(ds.xVec, dtype=np.float64), np.asarray(ds.zVec, dtype=np.float64)
+    qx, qz = np.tile(xv, len(zv)), np.repeat(zv, len(xv))
+    return models, qx, np.full(qx.shape, 100.0), qz
+
+
+def posterior_maps(tt, ctx, ds):
+    """SURVEY 8f row 2, plot_model_hist (MCsub.jl:753-781): every node's
+    v_nearest value in every saved model, then mean and std over the models
+    (td_rasterize, posterior_inputs).  Its CPU leg is timed in cpu_baseline."""
+    models, qx, qy, qz = posterior_inputs(tt, ds)
+    ncells = len(models[0][0])
+    ctx.rasterize(models[:2], qx, qy, qz)  # warm
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.rasterize(models, qx, qy, qz)
+    el = (time.perf_counter() - t0) / reps
+    return {"nodes": int(len(qx)), "models": len(models), "cells": ncells, "ms_per_section": round(el * 1e3, 3),
+            "node_model_pairs_per_s": round(len(qx) * len(models) / el, 1),
+            "nn_pair_evals_per_s_equiv": round(float(len(qx)) * ncells * len(models) / el, 1)}
+
+
+def trilinear_inputs(tt, grid=(120, 70, 40), seed=3):
+    """The ray points of the 10k synthetic stress rays and a seeded slowness
+    grid of `grid` knots covering them (pre_process_data.jl:34's workload)."""
+    s = tt.synthetic_rays(10000, seed=5)
+    px, py, pz = (a.T[~np.isnan(s.rayX.T)] for a in (s.rayX, s.rayY, s.rayZ))
+    rng = np.random.default_rng(seed)
+    lo = [min(a.min(), 0.0) - 1.0 for a in (px, py, pz)]
+    hi = [a.max() + 1.0 for a in (px, py, pz)]
+    xs, ys, zs = (np.sort(np.concatenate([[l, h], rng.uniform(l, h, n - 2)])) for l, h, n in zip(lo, hi, grid))
+    return xs, ys, zs, 1.0 / rng.uniform(5.0, 9.0, grid), px, py, pz
+
+
+def ingest_trilinear(tt):
+    """SURVEY 8f row 4, the ray points' slowness (Gridded(Linear()) of
+    load_3Dvel.jl:32): td_trilinear over every stress ray point; host buffers
+    in and out (PCIe included).  Its CPU leg is timed in cpu_baseline."""
+    from importlib import import_module
+    xs, ys, zs, vals, px, py, pz = trilinear_inputs(tt)
+    itp = import_module(tt.__name__ + ".ingest").Gridded(xs, ys, zs, vals, device=0)
+    itp(px[:1000], py[:1000], pz[:1000])  # warm
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        itp(px, py, pz)
+    el = (time.perf_counter() - t0) / reps
+    return {"points": int(len(px)), "grid": [len(xs), len(ys), len(zs)], "ms": round(el * 1e3, 3),
+            "points_per_s": round(len(px) / el, 1), "note": "host arrays in and out: PCIe-inclusive"}
+
+
 def host_cores():
     """The host cores this job may use: the box exports its CPU share in
     OMP_NUM_THREADS (16); os.cpu_count() reports the whole machine."""
@@ -509,7 +573,7 @@ def host_cores():
     return max(1, min(n if n > 0 else 16, os.cpu_count() or 1))
 
 
-def cpu_baseline(ds, model, seconds):
+def cpu_baseline(ds, model, seconds, tt=None):
     """The reference's structure on the host: one full evaluate per proposal
     (oracle/tstar_oracle.c, the scalar restatement of MCsub.jl:123-185), one
     chain per core as main_inversion.jl:15's pmap runs them.  Threads call the
@@ -541,7 +605,23 @@ def cpu_baseline(ds, model, seconds):
     n1, el1 = leg(1, seconds * 0.5)
     cores = host_cores()
     nc, elc = leg(cores, seconds * 0.5)
-    return {"value": round(nc / elc, 3), "unit": "proposals/s", "cores": cores, "kind": "port",
+    aux = {}
+    if tt is not None:  # the CPU legs of SURVEY 8f rows 2 and 4: the checker's numpy restatements, one core
+        from oracle import oracle_np
+
+        models, qx, qy, qz = posterior_inputs(tt, ds)
+        k = 10
+        t0 = time.perf_counter()
+        oracle_np.rasterize(models[:k], qx, qy, qz)
+        el = (time.perf_counter() - t0) * len(models) / k
+        aux["posterior_maps"] = {"ms_per_section": round(el * 1e3, 1), "cores": 1, "kind": "port (numpy)",
+                                 "sample": "%d of the %d models, scaled" % (k, len(models))}
+        xs, ys, zs, vals, px, py, pz = trilinear_inputs(tt)
+        t0 = time.perf_counter()
+        oracle_np.trilinear(xs, ys, zs, vals, px, py, pz)
+        aux["ingest_trilinear"] = {"ms": round((time.perf_counter() - t0) * 1e3, 1), "cores": 1,
+                                   "kind": "port (numpy)", "sample": "all %d points" % len(px)}
+    return {"value": round(nc / elc, 3), "unit": "proposals/s", "cores": cores, "kind": "port", "aux": aux,
             "single_core_value": round(n1 / el1, 3),
             "sample": "full evaluates (oracle/tstar_oracle.c, scalar FP64, -O2) of the same 381-ray x %d-cell "
                       "model, one chain per core: %d in %.1f s on %d cores, %d in %.1f s on 1 core; the reference "
