@@ -525,11 +525,17 @@ def posterior_maps(tt, ctx, ds):
     ncells = len(models[0][0])
     ctx.rasterize(models[:2], qx, qy, qz)  # warm
     reps = 3
+    ctx.timing(enable=True, reset=True)
     t0 = time.perf_counter()
     for _ in range(reps):
         ctx.rasterize(models, qx, qy, qz)
     el = (time.perf_counter() - t0) / reps
+    nl, kms = ctx.timing(kernel="raster_brute")
+    ctx.timing(enable=False)
     return {"nodes": int(len(qx)), "models": len(models), "cells": ncells, "ms_per_section": round(el * 1e3, 3),
+            "kernel_ms_per_section": round(kms / max(nl, 1), 4) if nl else None,
+            "note": "ms_per_section: the whole call from host arrays (cells packed into pinned memory, one copy); "
+                    "kernel: every model at every node in one launch (k_raster_brute)",
             "node_model_pairs_per_s": round(len(qx) * len(models) / el, 1),
             "nn_pair_evals_per_s_equiv": round(float(len(qx)) * ncells * len(models) / el, 1)}
 

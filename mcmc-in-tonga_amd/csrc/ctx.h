@@ -56,6 +56,10 @@ struct td_ctx {
     size_t raster_cap = 0;
     int *raster_i = nullptr;
     int64_t raster_i_cap = 0;
+    int64_t *raster_off = nullptr;      // td_rasterize: the models' cell offsets (batched search)
+    int64_t raster_off_cap = 0;
+    double *h_raster = nullptr;         // td_rasterize: pinned staging of queries and cells
+    size_t h_raster_cap = 0;
     double cell_lo[3] = {0, 0, 0}, cell_hi[3] = {0, 0, 0};  // box of the uploaded cells (NaN skipped)
     int nn_method = 0;                  // 0 auto, 1 brute force, 2 bucket grid (tdt_set_nn_method)
     void *chain_desc = nullptr;         // device array of chain descriptors (td_chain_run_batch)

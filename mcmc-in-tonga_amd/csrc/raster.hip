@@ -66,6 +66,74 @@ __device__ double julia_mapreduce_seq_blocks(F f, int n) {
     return vals[0];
 }
 
+// Every model at every node in ONE launch (the section's nodes are few; one
+// launch group per model cost ~80 us of launches and host work per model):
+// grid (node chunks, models).  A workgroup stages its model's cells through LDS
+// in chunks (x, y, z SoA), each lane keeps its node's running (distance, index)
+// with v_nearest's strict '<' in index order (MCsub.jl:250-258: the first
+// minimum wins, only distances below the 1e9 sentinel count; NaN never wins);
+// groups of 8 cells take one v_min per distance and look the index up only
+// when the group beats the running best.  The value is zeta of the winner, or
+// 0.0 when none (MCsub.jl:249).
+constexpr int kRasterThreads = 256;
+constexpr int kRasterChunk = 2048;  // cells per LDS chunk: 48 KB
+__global__ __launch_bounds__(kRasterThreads) void k_raster_brute(const int64_t *__restrict__ cell_off,
+                                                                 const double *__restrict__ cells, int64_t cs,
+                                                                 const double *__restrict__ q, int nq,
+                                                                 double *__restrict__ values) {
+    __shared__ double sx[kRasterChunk], sy[kRasterChunk], sz[kRasterChunk];
+    const int m = blockIdx.y;
+    const long a = (long)cell_off[m];
+    const int nc = (int)(cell_off[m + 1] - a);
+    const int node = blockIdx.x * kRasterThreads + threadIdx.x;
+    const int nd = min(node, nq - 1);
+    const double x = q[nd], y = q[nq + nd], z = q[2 * (long)nq + nd];
+    double bd = kSentinel;
+    int bi = -1;
+    for (int c0 = 0; c0 < nc; c0 += kRasterChunk) {
+        const int n = min(kRasterChunk, nc - c0);
+        __syncthreads();  // the previous chunk is read
+        for (int j = threadIdx.x; j < n; j += kRasterThreads) {
+            sx[j] = cells[a + c0 + j];
+            sy[j] = cells[cs + a + c0 + j];
+            sz[j] = cells[2 * cs + a + c0 + j];
+        }
+        __syncthreads();
+        int j = 0;
+        for (; j + 8 <= n; j += 8) {
+            double dg[8], mg;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                // (mx[i]-x)^2 + (my[i]-y)^2 + (mz[i]-z)^2, MCsub.jl:254, left to right, unfused
+                const double dx = sx[j + u] - x, dy = sy[j + u] - y, dz = sz[j + u] - z;
+                double d = dx * dx;
+                d = d + dy * dy;
+                d = d + dz * dz;
+                dg[u] = d;
+                mg = u == 0 ? d : fmin(mg, d);  // fmin: a NaN distance never becomes the minimum
+            }
+            if (mg < bd) {  // strict: NaN never wins
+                int f = 7;
+#pragma unroll
+                for (int u = 7; u >= 0; --u) f = dg[u] == mg ? u : f;
+                bd = mg;
+                bi = c0 + j + f;
+            }
+        }
+        for (; j < n; ++j) {
+            const double dx = sx[j] - x, dy = sy[j] - y, dz = sz[j] - z;
+            double d = dx * dx;
+            d = d + dy * dy;
+            d = d + dz * dz;
+            if (d < bd) {
+                bd = d;
+                bi = c0 + j;
+            }
+        }
+    }
+    if (node < nq) values[(long)m * nq + node] = bi >= 0 ? cells[3 * cs + a + bi] : 0.0;
+}
+
 __global__ __launch_bounds__(256) void k_raster_stats(const double *__restrict__ values, int nmodels, int nq,
                                                       double *__restrict__ mean, double *__restrict__ sd) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -117,17 +185,29 @@ extern "C" int td_rasterize(td_ctx *ctx, int64_t nmodels, const int64_t *cell_of
     double *dq = ctx->raster, *dc = dq + 3 * nq, *dv = dc + 4 * std::max<int64_t>(total, 1), *dm = dv + nmodels * nq,
            *ds = dm + nq;
     const int64_t cs = std::max<int64_t>(total, 1);  // SoA stride of the cells
-    std::vector<double> h(3 * (size_t)nq + 4 * (size_t)cs);
-    std::memcpy(h.data(), qx, sizeof(double) * (size_t)nq);
-    std::memcpy(h.data() + nq, qy, sizeof(double) * (size_t)nq);
-    std::memcpy(h.data() + 2 * nq, qz, sizeof(double) * (size_t)nq);
-    double *hc = h.data() + 3 * nq;
+    // packed into a pinned staging block (reused across calls), then one DMA copy: pageable
+    // copies of these sizes run at ~1 GB/s here
+    const size_t nh = 3 * (size_t)nq + 4 * (size_t)cs;
+    if (nh > ctx->h_raster_cap) {
+        if (ctx->h_raster) (void)hipHostFree(ctx->h_raster);
+        ctx->h_raster = nullptr;
+        ctx->h_raster_cap = 0;
+        TD_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_raster), sizeof(double) * nh, hipHostMallocDefault));
+        ctx->h_raster_cap = nh;
+    }
+    TD_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the staging block may still feed a previous copy
+    double *h = ctx->h_raster;
+    std::memcpy(h, qx, sizeof(double) * (size_t)nq);
+    std::memcpy(h + nq, qy, sizeof(double) * (size_t)nq);
+    std::memcpy(h + 2 * nq, qz, sizeof(double) * (size_t)nq);
+    double *hc = h + 3 * nq;
     if (total > 0) {
         std::memcpy(hc, xCell, sizeof(double) * (size_t)total);
         std::memcpy(hc + cs, yCell, sizeof(double) * (size_t)total);
         std::memcpy(hc + 2 * cs, zCell, sizeof(double) * (size_t)total);
         std::memcpy(hc + 3 * cs, zeta, sizeof(double) * (size_t)total);
     }
+    TD_HIP(ctx, hipMemcpyAsync(dq, h, sizeof(double) * nh, hipMemcpyHostToDevice, ctx->stream));
     if (nq > ctx->raster_i_cap) {  // nearest-cell indices (not returned)
         if (ctx->raster_i) (void)hipFree(ctx->raster_i);
         ctx->raster_i = nullptr;
@@ -135,9 +215,27 @@ extern "C" int td_rasterize(td_ctx *ctx, int64_t nmodels, const int64_t *cell_of
         TD_HIP(ctx, hipMalloc(&ctx->raster_i, sizeof(int) * (size_t)nq));
         ctx->raster_i_cap = nq;
     }
-    TD_HIP(ctx, hipMemcpyAsync(dq, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, ctx->stream));
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
-    for (int64_t k = 0; k < nmodels; ++k) {
+    // a section's few nodes: every model in one brute-force launch; many nodes: per model,
+    // the evaluate path's search (the bucket grid from kGridMinCells cells)
+    const bool batched = nq * (total / std::max<int64_t>(nmodels, 1)) <= (int64_t)1 << 28 && nmodels <= 65535;
+    if (batched) {
+        if (nmodels + 1 > ctx->raster_off_cap) {
+            if (ctx->raster_off) (void)hipFree(ctx->raster_off);
+            ctx->raster_off = nullptr;
+            ctx->raster_off_cap = 0;
+            TD_HIP(ctx, hipMalloc(&ctx->raster_off, sizeof(int64_t) * (size_t)(nmodels + 1)));
+            ctx->raster_off_cap = nmodels + 1;
+        }
+        TD_HIP(ctx, hipMemcpyAsync(ctx->raster_off, cell_off, sizeof(int64_t) * (size_t)(nmodels + 1),
+                                   hipMemcpyHostToDevice, ctx->stream));
+        hipEvent_t t0 = tm ? tm->begin(ctx->stream) : nullptr;
+        hipLaunchKernelGGL(k_raster_brute, dim3((unsigned)((nq + kRasterThreads - 1) / kRasterThreads), (unsigned)nmodels),
+                           dim3(kRasterThreads), 0, ctx->stream, ctx->raster_off, dc, cs, dq, (int)nq, dv);
+        if (tm) tm->end("raster_brute", t0, ctx->stream);
+        TD_HIP(ctx, hipGetLastError());
+    }
+    for (int64_t k = 0; k < (batched ? 0 : nmodels); ++k) {
         const int64_t a = cell_off[k], nc = cell_off[k + 1] - a;
         double *out = dv + k * nq;
         hipError_t e;

@@ -61,3 +61,33 @@ def test_plot_model_hist_sections(tt, ds):
     mk = maps[("xy", 100)]
     assert mk["mean"].shape == (len(xv), len(yv))
     assert np.array_equal(np.isnan(mk["masked"]), mk["std"] > 5)
+
+
+def test_batched_search_ties_nan_and_chunks(tt, ctx):
+    """A section's nodes take the all-models launch (k_raster_brute): cells
+    staged in 2048-cell chunks, so duplicated cells far apart in index (ties
+    across chunks: the lower index wins), NaN cells, an empty model, cells
+    beyond the 1e9 sentinel distance and nodes on cell sites."""
+    rng = np.random.default_rng(5)
+    base = tt.random_model(5000, 55).cells()
+    x, y, z, ze = (a.copy() for a in base)
+    x[4000:4600], y[4000:4600], z[4000:4600] = x[100:700], y[100:700], z[100:700]  # chunk 0 vs chunk 1
+    ze[4000:4600] = ze[100:700] + 1.0
+    x[::97] = np.nan
+    far = (np.full(50, 4e4), np.full(50, 4e4), np.full(50, 4e4), np.arange(50.0))  # d >= 1e9: never counts
+    empty = (np.zeros(0), np.zeros(0), np.zeros(0), np.zeros(0))
+    qx = np.concatenate([rng.uniform(-100, 1100, 500), x[100:300]])
+    qy = np.concatenate([rng.uniform(-200, 500, 500), y[100:300]])
+    qz = np.concatenate([rng.uniform(-10, 700, 500), z[100:300]])
+    qx[::50] = np.nan
+    check(ctx, [(x, y, z, ze), far, empty, base, tt.random_model(2048, 9).cells(), tt.random_model(2049, 10).cells()],
+          qx, qy, qz)
+
+
+def test_many_nodes_take_the_per_model_search(tt, ctx):
+    """Nodes x cells beyond the batched launch's budget: one search per model
+    (the evaluate path's bucket grid), the same answer."""
+    rng = np.random.default_rng(6)
+    n = 60000
+    qx, qy, qz = rng.uniform(-100, 1100, n), rng.uniform(-200, 500, n), rng.uniform(-10, 700, n)
+    check(ctx, models_of(tt, [5000, 4500], 400), qx, qy, qz)
