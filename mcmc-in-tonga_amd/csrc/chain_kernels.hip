@@ -380,6 +380,8 @@ __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf,
     BucketEntry e[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) e[u] = d.buckets[b * kBucketCap + grp * 4 + u];
+    // every cell outside the 3x3x3 block is at least sqrt(lb) away: computed while the loads fly
+    const double lb = grid_block_lb(G, x, y, z, 1);
     double bd = kSentinel;
     int bs = -1;
     bool tie = false;
@@ -421,8 +423,6 @@ __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf,
     const bool any_over = __ballot(overfull) != 0ull;
     res.s = found ? __builtin_amdgcn_readlane(bs, win) : -1;
     res.z = found ? readlane_f64(bz, win) : 0.0;
-    // every cell outside the 3x3x3 block is at least sqrt(lb) away
-    const double lb = grid_block_lb(G, x, y, z, 1);
     res.proven = !ovf && !tied && !any_over && res.d < lb;
     return res;
 }
