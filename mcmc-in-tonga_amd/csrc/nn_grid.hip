@@ -123,6 +123,7 @@ __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, 
     // the 3x3x3 block (one bucket per lane), then the 5x5x5 one (four per lane)
     for (int R = 1; R <= 2 && !proven; ++R) {
         const int W = 2 * R + 1, nbk = W * W * W;
+        const double lb = grid_block_lb(G, x, y, z, R);  // independent of the loads: computed while they fly
         bd = kSentinel;
         bx = INT_MAX;
         bool over = false;
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, 
         half_min(bd, bx);
         const unsigned long long ov = __ballot(over);
         const bool any_over = ((ov >> (threadIdx.x & 32)) & 0xffffffffull) != 0ull;
-        proven = !any_over && bd < grid_block_lb(G, x, y, z, R);  // nothing outside can tie or win
+        proven = !any_over && bd < lb;  // nothing outside can tie or win
     }
     if (!proven) {  // rare: every cell, the same half-wave (index order inside each lane)
         bd = kSentinel;
@@ -223,6 +224,7 @@ __global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx,
         cnt[u] = inb ? count[bb[u]] : 0;
         e[u] = ent[(long)bb[u] * kGridCap];
     }
+    const double lb = grid_block_lb(G, x, y, z, 1);  // independent of the loads: computed while they fly
     double bd = kSentinel;
     int bx = INT_MAX;
 #pragma unroll
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx,
     quad_lexmin(bd, bx);
     const int qsh = lane & ~(kGridLpp - 1);  // first lane of my quad
     const bool any_over = ((__ballot(over) >> qsh) & 0xfull) != 0ull;
-    const bool proven = p >= npts || (!any_over && bd < grid_block_lb(G, x, y, z, 1));
+    const bool proven = p >= npts || (!any_over && bd < lb);
     // points the block does not prove: the whole wave, one at a time
     unsigned long long need = __ballot(!proven && sub == 0);
     while (need) {
