@@ -1091,8 +1091,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             if (fwd) {
                 // ================= phase C: affected points =================
                 const int nt = sh.n_tiles;
-                const int rank_k = slot_k >= 0 ? d.rank[slot_k] : 0;
-                const double zeta_k = slot_k >= 0 ? d.czeta[slot_k] : 0.0;
+                // the selected cell's Julia position and value, known since the proposal was made:
+                // rank[slot_k] = p.index (slot_k = ord[p.index]), czeta[slot_k] = zeta_killed (no load)
+                const int rank_k = slot_k >= 0 ? (int)p.index : 0;
+                const double zeta_k = slot_k >= 0 ? zeta_killed : 0.0;
                 int seen = 0;
                 // one candidate point: captured (birth, move), re-valued (change) or orphaned
                 // (death, move: its nearest cell is the selected one)
