@@ -1068,8 +1068,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                             }
                     }
             }
-            if (action == tdchain::kDeath)  // deleteat! shift, staged before we know if it is accepted
-                for (int j = (int)p.index + 1 + tid; j < ncells; j += kChainThreads) d.order_tmp[j] = v.ord[j];
+            if (action == tdchain::kDeath) {  // deleteat! shift, staged before we know if it is accepted
+                const int sthr = query ? kChainThreads - 64 : kChainThreads;  // not the query wave: it starts at once
+                if (tid < sthr)
+                    for (int j = (int)p.index + 1 + tid; j < ncells; j += sthr) d.order_tmp[j] = v.ord[j];
+            }
             if (query && wv == kWaves - 1) {  // TD_inversion_function.jl:81 (birth), :146 (death)
                 const bool birth = action == tdchain::kBirth;
                 const Nearest r = wave_nearest(d, v, sh, lane, birth ? p.x : kx, birth ? p.y : ky, birth ? p.z : kz,
