@@ -1334,14 +1334,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // the rejection bound by a wide margin, the proposal is rejected
                 const int k0 = sh.k0;
                 if (!WALK && fwd && k0 < n && !nscript) {
+                    // the bound first: it does not depend on the sum (computed while the terms load)
+                    const double thr = tdchain::reject_bound(P, pp, sh.phi, czeta, zeta_killed, zetanew_death, sh.lnN);
+                    const double C0 = k0 > 0 ? v.prefix[k0 - 1] : 0.0;
                     double part = 0.0;
                     for (int k = k0 + lane; k < n; k += 64) part = part + v.term[k];
                     const double S = wave_sum_f64(part);
                     if (lane == 0) {
-                        const double C0 = k0 > 0 ? v.prefix[k0 - 1] : 0.0;
                         const double lb = (C0 + S) * (1.0 - 1e-9);
-                        const double thr =
-                            tdchain::reject_bound(P, pp, sh.phi, czeta, zeta_killed, zetanew_death, sh.lnN);
                         if (lb > thr + 1e-7 * (fabs(thr) + fabs(sh.phi)) + 1e-6)
                             __hip_atomic_store(&sh.early_reject, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
