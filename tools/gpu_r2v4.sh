@@ -2,4 +2,4 @@
 set -e
 mkdir -p gpurun_out
 timeout -k 10 300 python bench.py > gpurun_out/v4_bench.log 2>&1
-bash tools/profile.sh r02_v4 > gpurun_out/v4_prof.log 2>&1
+bash tools/profile.sh ${TAG:-r02_v5} > gpurun_out/v4_prof.log 2>&1 && bash tools/profile_aux.sh ${TAG:-r02_v5} >> gpurun_out/v4_prof.log 2>&1
