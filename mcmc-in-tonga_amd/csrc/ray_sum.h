@@ -107,7 +107,17 @@ __device__ double wave_ray_sum(int lane, const double *__restrict__ w, const Z &
         if (Q > 0 && lane < 32) {
             double acc = 0.0;
             if (lane == 0) acc = seg_term_z(w, zeta, s0) + seg_term_z(w, zeta, s0 + 1);
-            for (int q = 0; q < Q; ++q) acc = acc + seg_term_z(w, zeta, s0 + 2 + 32 * q + lane);
+            // four accumulator steps' terms loaded before any is added (one round of loads for
+            // a ray of up to 130 segments), then added in q order: the same association
+            for (int q0 = 0; q0 < Q; q0 += 4) {
+                double t[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    t[u] = q0 + u < Q ? seg_term_z(w, zeta, s0 + 2 + 32 * (q0 + u) + lane) : 0.0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (q0 + u < Q) acc = acc + t[u];
+            }
             acc_sh[lane] = acc;
         }
         if (lane < ntail) seq_sh[lane] = seg_term_z(w, zeta, s0 + tail0 + lane);
