@@ -16,16 +16,26 @@ all ranks / max-over-ranks wall time (weak scaling: one chain per GPU,
 independent chains, no data-path collective).
 
 Also reported:
-  roofline      -- k_chain_run (the only kernel in the timed region): the
-                   algorithmic bytes its proposals read (counted in-kernel)
-                   / its HIP-event time, against HBM peak.
+  roofline      -- k_chain_run (the only kernel in the timed region).  Its
+                   bound is LATENCY (one persistent workgroup per chain: a
+                   chain of dependent barriers and LDS/L2 round trips per
+                   proposal); `latency` gives the measured phase cycles.  The
+                   HBM line beside it prices what the incremental proposals
+                   actually read (counted in-kernel: tile boxes, candidate
+                   points, grid queries, re-summed ray points, chi^2 terms)
+                   against HBM peak; the full-evaluate bytes of SURVEY 8(d)
+                   are reported only as `reference_structure_bytes_per_proposal`.
   full_evaluate -- the drop-in td_evaluate path (brute-force P x N nearest
                    search, MCsub.jl:123-185) on the same model: latency and
-                   the FP64-VALU roofline of its dominant kernel nn_partial.
+                   the FP64-VALU roofline of its dominant kernel.
   cpu_baseline  -- the CPU oracle (scalar C restatement of evaluate), one
                    chain per host core of the job's share (and on 1 core),
                    ~--cpu-seconds in all: the reference's structure does one
                    full evaluate per proposal.
+At N > 1 ranks every rank also runs BASELINE config 4 (`config4_ranks`: one
+tempered replica per rank, a swap round every 10 proposals through the
+allgather -- RCCL over xGMI) and config 5 (`stress_chains`: one 10k x 20k
+stress chain per rank).
 """
 import argparse
 import json
@@ -39,24 +49,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
-# A latency floor for one chain proposal: the phases' dependent steps
-# priced with the primitives measured on the MI355X (tools/microbench.hip):
-# block barrier 350 cycles, dependent L2 hit 220, LDS round trip 90, FP64 add 30.
-LATENCY_FLOOR_MODEL = {
-    "B tile pass": (1, 0, 2, 0),       # (barriers, L2 trips, LDS trips, dependent FP64 ops)
-    "C points": (1, 1, 3, 8),
-    "D orphans (death, move: half)": (0.5, 1, 1.5, 6),
-    "E ray sums": (1, 1, 2, 10),
-    "F chi2 tail + decision": (1, 0, 2, 58 + 10),  # ~58-term tail added in order, 10 ops for alpha
-    "G commit + next proposal": (2, 0, 2, 0),
-}
-LATENCY_PRICES = (350.0, 220.0, 90.0, 30.0)
-CLOCK_GHZ = 2.4
-
-
-def latency_floor_us():
-    cyc = sum(sum(n * c for n, c in zip(v, LATENCY_PRICES)) for v in LATENCY_FLOOR_MODEL.values())
-    return cyc / (CLOCK_GHZ * 1e3)
 FP64_VALU_PEAK_TFLOPS = 78.6   # FP64 vector, FMA counted as 2 (spec)
 # the distance kernel may not use FMA (bit-exactness), so its roof is half that
 FP64_NOFMA_PEAK_TFLOPS = FP64_VALU_PEAK_TFLOPS / 2
@@ -86,33 +78,62 @@ def model_bytes(P, n, N):
     return 24 * P + 8 * S + 32 * N + 24 * n
 
 
-def chain_roofline(kernel, bytes_per_proposal, proposals_per_launch, avg_launch_s, counted_bytes_per_launch,
+def chain_roofline(kernel, ref_bytes_per_proposal, proposals_per_launch, avg_launch_s, counted_bytes_per_launch,
                    traffic_key, match):
-    """roofline block of a chain kernel: `achieved` = SURVEY 8(d) model bytes
-    per launch / the launch's HIP-event time; beside it the fraction by the
-    kernel's own in-kernel byte count and by the PMC-measured HBM traffic
-    (committed profile of the same command, `traffic_source`)."""
-    per_launch = bytes_per_proposal * proposals_per_launch
-    achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    out = {"kernel": kernel, "bound": "hbm", "limiter": "latency: one persistent workgroup per chain (dependent "
-                                                        "barriers and L2/LDS round trips), DESIGN.md 4.2",
-           "bytes_model": "SURVEY 8(d) 24P+8S+32N+24n = %d B per proposal" % bytes_per_proposal,
+    """roofline block of a chain kernel.  bound = latency.
+    The HBM line: `achieved` = the bytes the incremental proposals read,
+    counted in-kernel (tile boxes 32 B per tested tile, 36 B per candidate
+    point, 27 x 8 x 32 B per grid query, 17 B per re-summed ray point, 28 B
+    per chi^2 term), per launch / the launch's HIP-event time; `traffic` =
+    the PMC-measured HBM bytes per launch from the committed rocprofv3
+    profile of the same command (`traffic_source`).  SURVEY 8(d)'s
+    full-evaluate bytes are what the reference's structure would read per
+    proposal: reported, never priced against the peak."""
+    achieved = counted_bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    out = {"kernel": kernel, "bound": "latency",
+           "limiter": "one persistent workgroup per chain: dependent barriers and LDS/L2 round trips "
+                      "(DESIGN.md 4.2); HBM line below",
            "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None, "traffic_source": None,
-           "traffic_measured_in_this_run": False, "algorithmic_bytes_per_launch": round(per_launch, 1),
+           "bytes_model": "in-kernel count of what the incremental proposals read (tile boxes, candidate points, "
+                          "grid queries, re-summed ray points, chi^2 terms)",
+           "algorithmic_bytes_per_launch": round(counted_bytes_per_launch, 1),
+           "reference_structure_bytes_per_proposal": ref_bytes_per_proposal,
            "proposals_per_launch": proposals_per_launch, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-           "us_per_proposal": round(avg_launch_s / max(proposals_per_launch, 1) * 1e6, 4),
-           "in_kernel_bytes_per_launch": round(counted_bytes_per_launch, 1),
-           "frac_in_kernel_count": round(counted_bytes_per_launch / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6)
-           if avg_launch_s > 0 else 0.0}
+           "us_per_proposal": round(avg_launch_s / max(proposals_per_launch, 1) * 1e6, 4)}
     if match:
         tr, src, prof_us = measured_traffic(traffic_key)
         if tr is not None:
             out["traffic"], out["traffic_source"] = tr, src
-            out["frac_measured_traffic"] = round(tr / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6)
+            out["traffic_frac_of_peak"] = round(tr / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6)
             if prof_us:
                 out["profile_avg_launch_ms"] = round(prof_us / 1e3, 4)
     return out
+
+
+PHASES = ["loop top", "B tiles + query", "C points", "D orphans", "E ray sums", "F chi2 + decision", "G commit + next"]
+
+
+def phase_cycles(tt, ch, iters):
+    """The chain's s_memtime phase stamps (a diagnostic mode of k_chain_run,
+    DESIGN.md 4.2) over `iters` more proposals, after the timed region:
+    cycles per proposal of each phase and the stamp clock (cycles / wall s)."""
+    import ctypes
+
+    L = tt.lib()
+    a, b = (ctypes.c_int64 * 80)(), (ctypes.c_int64 * 80)()
+    L.tdt_chain_profile(ch.h, 1, a)
+    t0 = time.perf_counter()
+    ch.run(iters)
+    el = time.perf_counter() - t0
+    L.tdt_chain_profile(ch.h, 0, b)
+    cyc = [float(b[k] - a[k]) for k in range(7)]
+    cyc[6] += float((b[12] - a[12]) + (b[13] - a[13]))
+    tot = sum(cyc)
+    return {"proposals": iters, "cycles_per_proposal": round(tot / iters, 1),
+            "phases": {p: round(c / iters, 1) for p, c in zip(PHASES, cyc)},
+            "stamp_clock_ghz": round(tot / el / 1e9, 3), "us_per_proposal_stamped": round(el / iters * 1e6, 3),
+            "note": "stamped run (+~5 %), after the timed region; per-phase cycles are the latency yardstick"}
 
 
 def parse():
@@ -140,6 +161,9 @@ def parse():
                     help="skip the config-4 block (8 tempered replicas x 2000 cells, swap every 10, one GPU)")
     ap.add_argument("--no-stress", action="store_true",
                     help="skip the config-5 stress block (10k synthetic rays x 20k cells)")
+    ap.add_argument("--config4-rounds", type=int, default=300, help="timed swap rounds of the config-4 blocks")
+    ap.add_argument("--stress-iters", type=int, default=2000, help="timed proposals of the stress chain(s)")
+    ap.add_argument("--no-phases", action="store_true", help="skip the stamped phase-cycle run")
     return ap.parse_args()
 
 
@@ -263,17 +287,20 @@ def main():
                                    bytes_per_launch, "k_chain_run/single",
                                    C == 1 and ladder is None and N == 5000 and a.iters_per_step == 5000),
     }
-    if C == 1:  # the bound that applies to one chain: its chain of dependent steps
-        us = avg_s / max(a.iters_per_step, 1) * 1e6
-        fl = latency_floor_us()
-        out["roofline"]["latency_floor"] = {
-            "us_per_proposal": round(fl, 3), "achieved_us_per_proposal": round(us, 3), "frac": round(fl / us, 4),
-            "model": "sum over phases B-G of barriers x 350 + dependent L2 trips x 220 + LDS trips x 90 + "
-                     "dependent FP64 ops x 30 cycles at 2.4 GHz (microbench.hip prices; DESIGN.md 4.2): %s"
-                     % {k: v for k, v in LATENCY_FLOOR_MODEL.items()}}
+    if C == 1 and ladder is None and not a.no_phases:  # the latency yardstick, measured after the timed region
+        out["roofline"]["latency"] = phase_cycles(tt, chains[0], min(a.iters_per_step, 5000))
     if ladder is not None:
         out["tempering"] = {"replicas": ladder.R, "temps": [round(t, 4) for t in ladder.temps],
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
+    if dist is not None and a.config4:  # every rank: config 4, one tempered replica per rank, RCCL allgather
+        c4 = config4_ranks(tt, ds, tt.Exchange(dist, coll_dev), dist, coll_dev, rank, world, local,
+                           rounds=a.config4_rounds)
+        if rank == 0:
+            out["config4_ranks"] = c4
+    if dist is not None and not a.no_stress:  # every rank: config 5, one stress chain per rank
+        sc = stress_chains(tt, dist, coll_dev, rank, world, local, a.stress_iters)
+        if rank == 0:
+            out["stress_chains"] = sc
     if dist is not None and not a.no_stress:  # every rank: the stress evaluate split over the ranks' rays
         sh = stress_sharded(tt, tt.Exchange(dist, coll_dev), dist, coll_dev, local)
         if rank == 0:
@@ -283,9 +310,9 @@ def main():
     if rank == 0 and not a.no_dropin:
         out["dropin"] = dropin(tt, ds, model)
     if rank == 0 and not a.no_stress:
-        out["stress"] = stress(tt)
+        out["stress"] = stress(tt, a.stress_iters)
     if rank == 0 and a.config4:
-        out["config4_tempering"] = tempering_config4(tt, ctx, ds)
+        out["config4_tempering"] = tempering_config4(tt, ctx, ds, rounds=a.config4_rounds)
     if rank == 0 and not a.no_full_evaluate:  # SURVEY 8f rows 2 and 4, measured beside their CPU restatements
         out["posterior_maps"] = posterior_maps(tt, ctx, ds)
         out["ingest_trilinear"] = ingest_trilinear(tt)
@@ -314,9 +341,7 @@ def tempering_config4(tt, ctx, ds, nrep=8, ncells=2000, swap_every=10, rounds=30
     proposals; the replicas run in one td_chain_run_batch launch per round, the
     allgather is the identity in one process (the N-GPU runs put one rank per
     GPU and gather over RCCL: tests/test_gpu_config4.py checks the two agree)."""
-    prm = tt.define_TDstructrure().replace(max_cells=2 * ncells)
-    chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=100 + g, chain=1 + g), tt.random_model(ncells, 100 + g))
-              for g in range(nrep)]
+    chains = config4_replicas(tt, ctx, ds, 0, nrep, ncells)
     lad = tt.TemperingLadder(chains, tmax=8.0, seed=4242)
     for _ in range(20):
         lad.step(swap_every)
@@ -335,6 +360,90 @@ def tempering_config4(tt, ctx, ds, nrep=8, ncells=2000, swap_every=10, rounds=30
            "cold_phi": chains[lad.cold_local()].stats()["phi"]}
     for c in chains:
         c.close()
+    return res
+
+
+def config4_replicas(tt, ctx, ds, first, count, ncells=2000):
+    """BASELINE config 4's replicas g = first .. first + count - 1: seed
+    100 + g, chain id 1 + g, model random_model(ncells, 100 + g), max_cells
+    2 ncells (tests/tempering_worker.py builds the same)."""
+    prm = tt.define_TDstructrure().replace(max_cells=2 * ncells)
+    return [tt.Chain(ctx, tt.chain_params(prm, ds, seed=100 + g, chain=1 + g), tt.random_model(ncells, 100 + g))
+            for g in range(first, first + count)]
+
+
+def config4_ranks(tt, ds, ex, dist, coll_dev, rank, world, device, swap_every=10, rounds=300, warm=20):
+    """BASELINE config 4 across the ranks: one tempered replica per rank
+    (replica g = rank), geometric T in [1, 8] over the world, a swap round
+    every 10 proposals: the replica's launch, the allgather of every rank's
+    phi (torch.distributed: RCCL over xGMI with one rank per GPU) and the
+    same swap decision on every rank.  value = all ranks' proposals / the
+    max-over-ranks time.  Rank 0 then replays the same ladder in ONE process
+    (all `world` replicas on its GPU, identity gather): the swap traces'
+    digests must be equal."""
+    import torch
+
+    ctx = tt.TdContext.from_datastruct(ds, device=device)
+    chains = config4_replicas(tt, ctx, ds, rank, 1)
+    lad = tt.TemperingLadder(chains, ex, tmax=8.0, seed=4242)
+    for _ in range(warm):
+        lad.step(swap_every)
+    g0 = lad.gather_s
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        lad.step(swap_every)
+    el = time.perf_counter() - t0
+    gat = (lad.gather_s - g0) / rounds
+    t = torch.tensor([el, gat], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el, gat_max = float(t[0].item()), float(t[1].item())
+    digest = lad.trace_digest()
+    res = {"replicas": world, "ranks": world, "cells": 2000, "swap_every": swap_every, "rounds": rounds,
+           "proposals_per_s": round(world * swap_every * rounds / el, 1), "ms_per_round": round(el / rounds * 1e3, 4),
+           "allgather_us_per_round": round(gat * 1e6, 2), "allgather_us_per_round_max_rank": round(gat_max * 1e6, 2),
+           "temps": [round(x, 4) for x in lad.temps], "swap_rates": [round(r, 3) for r in lad.swap_rates()],
+           "collective": "allgather of 8 B per rank (%s)" % ("RCCL" if coll_dev == "cuda" else "gloo")}
+    for c in chains:
+        c.close()
+    if rank == 0:  # the one-process ladder of the same replicas
+        ref = config4_replicas(tt, ctx, ds, 0, world)
+        lad1 = tt.TemperingLadder(ref, tmax=8.0, seed=4242)
+        for _ in range(warm + rounds):
+            lad1.step(swap_every)
+        res["trace_sha256"] = digest
+        res["trace_matches_single_process"] = lad1.trace_digest() == digest
+        for c in ref:
+            c.close()
+    ctx.close()
+    return res
+
+
+def stress_chains(tt, dist, coll_dev, rank, world, device, iters):
+    """BASELINE config 5 across the ranks: 10k synthetic rays x 20k cells,
+    one chain per rank (seed 77 + rank), `iters` proposals each; value = all
+    ranks' proposals / the max-over-ranks time (weak scaling)."""
+    import torch
+
+    ds = tt.synthetic_rays(10000, seed=5)
+    ctx = tt.TdContext.from_datastruct(ds, device=device)
+    prm = tt.define_TDstructrure().replace(max_cells=40000)
+    ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=77 + rank, chain=1 + rank), tt.random_model(20000, 5))
+    ch.run(200)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    ch.run(iters)
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    res = {"chains": world, "rays": int(ctx.n), "cells": 20000, "iters_per_chain": iters,
+           "proposals_per_s": round(world * iters / el, 1), "per_chain_proposals_per_s": round(iters / el, 1),
+           "phi_rank0": ch.stats()["phi"]}
+    ch.close()
+    ctx.close()
     return res
 
 
@@ -359,8 +468,6 @@ def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3):
     avg_s = kms / 1e3 / max(launches, 1)
     roof = chain_roofline("k_chain_run (grid = %d chains)" % C, model_bytes(int(ctx.P), int(ctx.n), len(model.xCell)),
                           C * iters, avg_s, nbytes / max(launches, 1), "k_chain_run/many256", C == 256 and iters == 5000)
-    roof["note"] = ("the full-evaluate byte model exceeds HBM peak here: the incremental kernel does not read what a "
-                    "full evaluate reads (its working set stays in LDS / L2), see frac_measured_traffic")
     return {"chains": C, "proposals_per_s": round(value, 1), "per_chain_proposals_per_s": round(value / C, 1),
             "ms_per_launch": round(kms / max(launches, 1), 4), "iters_per_launch": iters, "roofline": roof}
 

@@ -83,6 +83,17 @@ int td_timing_get(td_ctx *ctx, const char *kernel, int64_t *launches, double *to
  * (TD_inversion_function.jl:252-261); n values. */
 int td_set_sigma(td_ctx *ctx, const double *allSig);
 
+/* td_evaluate's incremental path (below): 2 (default) = a resident kernel
+ * answers every call through a mailbox in pinned host memory; 1 = one launch
+ * per call; 0 = every call a full evaluate.  A resident kernel occupies its
+ * stream's hardware queue, so one kept alive while the caller runs other GPU
+ * work (another context, a collective on another stream) can hold that work
+ * back until its 200 ms idle watchdog.  The library stops this thread's
+ * resident kernels before any call that launches other work; a caller that
+ * interleaves its OWN GPU work with td_evaluate calls (e.g. an allgather
+ * between evaluates: a ray-sharded run) should select mode 1. */
+int td_set_incremental(td_ctx *ctx, int mode);
+
 /* ------------------------------------------------------------------------
  * evaluate -- replaces MCsub.jl:123-185 `evaluate(model, dataStruct,
  * TD_parameters)` (interp_style 1, MCsub.jl:326-327).
@@ -244,6 +255,26 @@ int td_chain_get_model(const td_chain *ch, double *xCell, double *yCell, double 
                        int64_t cap, int64_t *nCells, double *phi, double *ptS_out);
 /* Tempering: change the temperature between runs (swap step). */
 int td_chain_set_temperature(td_chain *ch, double temperature);
+
+/* ------------------------------------------------------------------------
+ * Resident tempering rounds (parallel tempering; the reference's
+ * chains are independent pmap workers, main_inversion.jl:15, so this is a new
+ * capability): DEVICE chains of one context run in ONE launch that stays
+ * resident across swap rounds.  td_rounds_run posts a round -- K proposals on
+ * every chain at the given temperatures -- and returns each chain's phi after
+ * it; the caller gathers the phis (across ranks: an allgather), decides the
+ * swaps and passes the new temperatures to the next td_rounds_run.  No
+ * launch per round; the launch returns by itself after 200 ms without a
+ * round (and is started again by the next one, with identical results).
+ * Every chain's trajectory equals td_chain_run of K proposals per round with
+ * td_chain_set_temperature between rounds.  Any other call on these chains
+ * (or any GPU work of this thread through this library) first ends the
+ * launch; td_chain_stats_get's accepted/proposed counts are current after
+ * that, phi and iterations after every round. */
+typedef struct td_rounds td_rounds;
+int td_rounds_create(td_rounds **out, td_chain *const *chains, int64_t nchains);
+int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out);
+int td_rounds_destroy(td_rounds *r);
 
 #ifdef __cplusplus
 }

@@ -50,6 +50,11 @@ int tdt_accept(const td_chain_params *prm, int action, double u_accept, double z
  * in LDS when they fit (the 381-ray configs); 1 keeps them in HBM, the path
  * larger geometries take.  Same results either way. */
 int tdt_chain_set_lds_mode(td_chain *ch, int mode);
+/* td_evaluate's resident server (incremental.cpp): sleep `ms` between the
+ * host's alive check and the post of every command, so the kernel's 200 ms
+ * idle watchdog can fire first (the race of a descheduled host thread).  The
+ * command must then be re-issued to a new launch with the same results.  0 = off. */
+int tdt_set_server_post_delay(int ms);
 /* The block-wide exact sequential sum (exact_sum.h, used for chi^2 over long
  * ray lists): prefix[k] = C0 + term[0] + ... + term[k] added strictly left to
  * right in FP64 (MCsub.jl:170-172).  *fast = 1 when the parallel path proved

@@ -12,7 +12,7 @@ Layers: L1 types/config (defstruct, config), L2 data (data),
 L3 forward model over the C ABI (forward -> libtdstar.so), L4 chain (chain).
 """
 from ._lib import TD_ENGINE_DEVICE, TD_ENGINE_DROPIN, TD_ENGINE_HOST, TdError, lib  # noqa: F401
-from .chain import Chain, TD_inversion_function, build_starting, chain_params, main_inversion, run_batch  # noqa: F401
+from .chain import Chain, TD_inversion_function, build_starting, chain_params, main_inversion, run_batch, run_chains  # noqa: F401,E501
 from .config import define_TDstructrure, parameters  # noqa: F401
 from .data import (CONFIGS, ak135_slowness, box, interp1, load_data_Tonga, lonlat2xy, pad_rays,  # noqa: F401
                    random_model, segments, synthetic_rays)

@@ -53,6 +53,10 @@ SIGNATURES = {
     "td_get_info": (ctypes.c_int, [_vp, ctypes.POINTER(TdInfo)]),
     "td_set_sigma": (ctypes.c_int, [_vp, _pd]),
     "td_misfit": (ctypes.c_int, [_vp, _i64, _pd, _pd, _pd, _pd, _pd]),
+    "td_set_incremental": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "td_rounds_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _i64]),
+    "td_rounds_run": (ctypes.c_int, [_vp, _i64, _pd, _pd]),
+    "td_rounds_destroy": (ctypes.c_int, [_vp]),
     "td_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "td_timing_reset": (ctypes.c_int, [_vp]),
     "td_timing_get": (ctypes.c_int, [_vp, ctypes.c_char_p, _pi64, _pd]),
@@ -89,6 +93,7 @@ SIGNATURES = {
                                             ctypes.POINTER(ctypes.c_int64), _pi32]),
     "tdt_wave_seq_sum": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _d, _pd, _pd, _pi32]),
     "tdt_set_incremental": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "tdt_set_server_post_delay": (ctypes.c_int, [ctypes.c_int]),
     "tdt_shadow_diag": (ctypes.c_int, [_vp, _pi64]),
     "tdt_shadow_profile": (ctypes.c_int, [_vp, _pi64]),
     "tdt_chi2": (ctypes.c_int, [_vp, _pd, ctypes.c_int, _pd]),

@@ -116,6 +116,36 @@ def run_batch(chains, iterations):
     check(lib().td_chain_run_batch(arr, len(chains), int(iterations)), chains[0].ctx.h)
 
 
+class Rounds:
+    """A resident tempering launch over DEVICE chains of one context
+    (td_rounds_*): ``run(K, temps)`` -> every chain's phi after K more
+    proposals at those temperatures; no launch per round."""
+
+    def __init__(self, chains):
+        self.chains = list(chains)
+        arr = (ctypes.c_void_p * len(self.chains))(*[c.h for c in self.chains])
+        h = ctypes.c_void_p()
+        check(lib().td_rounds_create(ctypes.byref(h), arr, len(self.chains)), self.chains[0].ctx.h)
+        self.h = h
+        self._phi = np.zeros(len(self.chains))
+
+    def run(self, K, temps):
+        t = f64(temps)
+        check(lib().td_rounds_run(self.h, int(K), ptr(t), ptr(self._phi)), self.chains[0].ctx.h)
+        return self._phi.copy()
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().td_rounds_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def build_starting(TD_parameters, dataStruct, seed=1, chain=1):
     """MCsub.jl:76-121 (log-uniform nCells, uniform cells, zeta ~ U(0, zeta_scale)),
     drawn by the chain's RNG; returns (model, dataStruct, valid)."""
@@ -151,65 +181,101 @@ def TD_inversion_function(TD_parameters, dataStruct, chain, seed=None, model=Non
     checkpoint's dataStruct is the caller's (it never changes: action 5 is
     unreachable, :72).  ``stop_after``: return after that iteration (testing a
     crash and resume)."""
-    from . import jld
+    drv = _ChainDriver(TD_parameters, dataStruct, chain, seed, model, engine, checkpoint_dir, verbose, temperature,
+                       stop_after)
+    while True:
+        k = drv.next_stretch()
+        if k is None:
+            return drv.finish()
+        drv.ch.run(k)
+        drv.after_stretch()
 
-    ctx = context_for(dataStruct)
-    seed = chain * 7919 + 1 if seed is None else seed
-    prm = chain_params(TD_parameters, dataStruct, seed=seed, chain=chain, temperature=temperature, engine=engine)
-    n_iter, keep = int(TD_parameters.n_iter), int(TD_parameters.keep_each)
-    B = float(TD_parameters.burn_in)
-    print_each = int(TD_parameters.print_each)
-    num_models = int((TD_parameters.n_iter - TD_parameters.burn_in) / TD_parameters.keep_each)  # :25
-    model_hist, it0, model_num, used_num = [], 1, 0, 0
-    ckpt = _latest_checkpoint(checkpoint_dir, chain) if checkpoint_dir else None
-    if ckpt is not None:  # :41-67 resume
-        c = jld.load_checkpoint(ckpt)
-        model = c["model"]
-        it0 = int(c["iter"]) + 1
-        if c["burnin"]:
-            model_hist, used_num, model_num = list(c["model_hist"]), c["saved"], c["model_num"]
-    prm.start_iter = it0  # the counter-based RNG continues exactly where the checkpoint stopped
-    ch = Chain(ctx, prm, model)
 
-    def current():
-        m = ch.model()
-        m.tS = dataStruct.tS
-        m.likelihood = ctx.likelihood_const if TD_parameters.debug_prior != 1 else 1.0
+class _ChainDriver:
+    """One chain of TD_inversion_function as a sequence of stretches: the
+    iterations between two bookkeeping points run in ONE device launch;
+    ``next_stretch`` says how many, ``after_stretch`` does the bookkeeping.
+    Several drivers can share launches (main_inversion: td_chain_run_batch)."""
+
+    def __init__(self, TD_parameters, dataStruct, chain, seed, model, engine, checkpoint_dir, verbose, temperature,
+                 stop_after):
+        from . import jld
+
+        self.jld = jld
+        self.prm_ref = TD_parameters
+        self.ds = dataStruct
+        self.chain = chain
+        self.ctx = ctx = context_for(dataStruct)
+        seed = chain * 7919 + 1 if seed is None else seed
+        prm = chain_params(TD_parameters, dataStruct, seed=seed, chain=chain, temperature=temperature, engine=engine)
+        self.n_iter, self.keep = int(TD_parameters.n_iter), int(TD_parameters.keep_each)
+        self.B = float(TD_parameters.burn_in)
+        self.print_each = int(TD_parameters.print_each)
+        self.num_models = int((TD_parameters.n_iter - TD_parameters.burn_in) / TD_parameters.keep_each)  # :25
+        self.model_hist, it0, self.model_num, self.used_num = [], 1, 0, 0
+        self.ckdir = checkpoint_dir
+        self.verbose = verbose
+        ckpt = _latest_checkpoint(checkpoint_dir, chain) if checkpoint_dir else None
+        if ckpt is not None:  # :41-67 resume
+            c = jld.load_checkpoint(ckpt)
+            model = c["model"]
+            it0 = int(c["iter"]) + 1
+            if c["burnin"]:
+                self.model_hist, self.used_num, self.model_num = list(c["model_hist"]), c["saved"], c["model_num"]
+        prm.start_iter = it0  # the counter-based RNG continues exactly where the checkpoint stopped
+        self.ch = Chain(ctx, prm, model)
+        self.last = self.n_iter if stop_after is None else min(self.n_iter, int(stop_after))
+        self.it = it0
+        self.nxt = None
+
+    def current(self):
+        m = self.ch.model()
+        m.tS = self.ds.tS
+        m.likelihood = self.ctx.likelihood_const if self.prm_ref.debug_prior != 1 else 1.0
         return m
 
-    last = n_iter if stop_after is None else min(n_iter, int(stop_after))
-    it = it0
-    while it <= last:
-        # run up to the next iteration with bookkeeping, in one device launch
-        nxt = last
-        if it < B:  # pre-burn-in: checkpoints every print_each (:289)
-            nxt = min(nxt, int(np.ceil(B)) - 1)
-        elif keep > 0:  # the next saved model: model_num + (nxt - it + 1) = 0 mod keep
-            nxt = min(nxt, it + (keep - model_num % keep) - 1)
-        if print_each > 0:
-            nxt = min(nxt, ((it + print_each - 1) // print_each) * print_each)
-        nxt = max(nxt, it)
-        ch.run(nxt - it + 1)
-        if nxt >= B:  # :276-288
-            model_num += nxt - it + 1
-            if keep > 0 and model_num % keep == 0:
-                used_num += 1
-                m = current()
-                model_hist.append(m)
-                if checkpoint_dir and ((100 * used_num / num_models) % 10 < 1e-9 or used_num == 1):
-                    os.makedirs(checkpoint_dir, exist_ok=True)
-                    name = "chain%d_iter%d_%r%%.jld" % (chain, nxt, 100 * float(nxt) / float(TD_parameters.n_iter))
-                    jld.save_checkpoint(os.path.join(checkpoint_dir, name), m, dataStruct, float(nxt), True,
-                                        model_hist, used_num, model_num)
-        elif checkpoint_dir and print_each > 0 and nxt % print_each == 0:  # :289-294
-            os.makedirs(checkpoint_dir, exist_ok=True)
-            name = "chain%d_iter%d_%d%%.jld" % (chain, nxt, int(100 * nxt / TD_parameters.n_iter))
-            jld.save_checkpoint(os.path.join(checkpoint_dir, name), current(), dataStruct, nxt, False)
-        if verbose and print_each > 0 and nxt % print_each == 0:  # :296-298
-            print("Chain #%d at %r%% with a phi of %r" % (chain, 100 * nxt / TD_parameters.n_iter, ch.stats()["phi"]))
-        it = nxt + 1
-    ch.close()
-    return model_hist
+    def next_stretch(self):
+        """Iterations to run up to the next one with bookkeeping (None: done)."""
+        it = self.it
+        if it > self.last:
+            return None
+        nxt = self.last
+        if it < self.B:  # pre-burn-in: checkpoints every print_each (:289)
+            nxt = min(nxt, int(np.ceil(self.B)) - 1)
+        elif self.keep > 0:  # the next saved model: model_num + (nxt - it + 1) = 0 mod keep
+            nxt = min(nxt, it + (self.keep - self.model_num % self.keep) - 1)
+        if self.print_each > 0:
+            nxt = min(nxt, ((it + self.print_each - 1) // self.print_each) * self.print_each)
+        self.nxt = max(nxt, it)
+        return self.nxt - it + 1
+
+    def after_stretch(self):
+        it, nxt, jld = self.it, self.nxt, self.jld
+        TD = self.prm_ref
+        if nxt >= self.B:  # :276-288
+            self.model_num += nxt - it + 1
+            if self.keep > 0 and self.model_num % self.keep == 0:
+                self.used_num += 1
+                m = self.current()
+                self.model_hist.append(m)
+                # used_num == 1 first: with n_iter == burn_in num_models is 0 (Julia gives Inf, no error)
+                if self.ckdir and (self.used_num == 1 or
+                                   (self.num_models > 0 and (100 * self.used_num / self.num_models) % 10 < 1e-9)):
+                    os.makedirs(self.ckdir, exist_ok=True)
+                    name = "chain%d_iter%d_%r%%.jld" % (self.chain, nxt, 100 * float(nxt) / float(TD.n_iter))
+                    jld.save_checkpoint(os.path.join(self.ckdir, name), m, self.ds, float(nxt), True,
+                                        self.model_hist, self.used_num, self.model_num)
+        elif self.ckdir and self.print_each > 0 and nxt % self.print_each == 0:  # :289-294
+            os.makedirs(self.ckdir, exist_ok=True)
+            name = "chain%d_iter%d_%d%%.jld" % (self.chain, nxt, int(100 * nxt / TD.n_iter))
+            jld.save_checkpoint(os.path.join(self.ckdir, name), self.current(), self.ds, nxt, False)
+        if self.verbose and self.print_each > 0 and nxt % self.print_each == 0:  # :296-298
+            print("Chain #%d at %r%% with a phi of %r" % (self.chain, 100 * nxt / TD.n_iter, self.ch.stats()["phi"]))
+        self.it = nxt + 1
+
+    def finish(self):
+        self.ch.close()
+        return self.model_hist
 
 
 def _ckpt_iter(f):
@@ -233,20 +299,48 @@ def delete_checkpoints(d):
         os.remove(f)
 
 
+def run_chains(TD_parameters, dataStruct, chains, engine=_lib.TD_ENGINE_DEVICE, checkpoint_dir=None,
+               verbose=False, seeds=None):
+    """``pmap(x -> TD_inversion_function(TD_parameters, dataStruct, x), chains)``
+    (main_inversion.jl:15) on this GPU: every chain's stretch between two
+    bookkeeping points runs in ONE td_chain_run_batch launch with the others
+    (one workgroup per chain, concurrently, as the reference's workers run);
+    chains whose stretches differ (resumed from different checkpoints) run in
+    separate launches.  Each chain's model_hist is the one TD_inversion_function
+    returns for it alone."""
+    chains = list(chains)
+    seeds = seeds or [None] * len(chains)
+    drv = [_ChainDriver(TD_parameters, dataStruct, c, s, None, engine, checkpoint_dir, verbose, 1.0, None)
+           for c, s in zip(chains, seeds)]
+    live = list(drv)
+    while live:
+        want = {}
+        for d in live:
+            k = d.next_stretch()
+            if k is not None:
+                want.setdefault(k, []).append(d)
+        live = [d for ds_ in want.values() for d in ds_]
+        for k, group in want.items():
+            run_batch([d.ch for d in group], k)
+            for d in group:
+                d.after_stretch()
+    return [d.finish() for d in drv]
+
+
 def main_inversion(TD_parameters=None, dataStruct=None, out="model.jld", checkpoint_dir=None,  # noqa: N803
                    engine=_lib.TD_ENGINE_DEVICE):
-    """main_inversion.jl:11-18: the chains (one after another on this GPU; one
-    rank per GPU for more, see tempering/bench), the posterior maps of
-    plot_model_hist (numbers only) and ``save(out, "model", models)`` in JLD.
-    Returns (models, maps)."""
+    """main_inversion.jl:11-18: the chains (concurrently on this GPU, one
+    td_chain_run_batch launch per stretch: run_chains; one rank per GPU for
+    more, see tempering/bench), the posterior maps of plot_model_hist (numbers
+    only) and ``save(out, "model", models)`` in JLD.  Returns (models, maps)."""
     from . import jld
     from .config import define_TDstructrure
     from .data import load_data_Tonga
     from .posterior import plot_model_hist
     TD_parameters = TD_parameters or define_TDstructrure()
     dataStruct = dataStruct or load_data_Tonga(TD_parameters)
-    models = [TD_inversion_function(TD_parameters, dataStruct, c, engine=engine, checkpoint_dir=checkpoint_dir)
-              for c in range(1, int(TD_parameters.n_chains) + 1)]
+    models = run_chains(TD_parameters, dataStruct, range(1, int(TD_parameters.n_chains) + 1), engine=engine,
+                        checkpoint_dir=checkpoint_dir)
     maps = plot_model_hist(models, dataStruct, TD_parameters, 20.0)
     if out:
         jld.save(out, models)

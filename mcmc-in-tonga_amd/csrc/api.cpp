@@ -390,6 +390,7 @@ int td_get_info(const td_ctx *ctx, td_info *info) {
 int td_set_sigma(td_ctx *ctx, const double *allSig) {
     if (!ctx || (!allSig && ctx->g.n > 0)) return set_err(ctx, TD_ERR_ARG, "td_set_sigma: NULL");
     TD_HIP(ctx, hipSetDevice(ctx->device));
+    servers_quiesce(nullptr);
     shadow_free(ctx);  // the shadow chain's chi^2 terms were for the old sigma
     ctx->sig_host.assign(allSig, allSig + ctx->g.n);
     ctx->likelihood = likelihood_constant(allSig, ctx->g.n);
@@ -409,6 +410,7 @@ int td_misfit(td_ctx *ctx, int64_t n, const double *ptS, const double *tS, const
         return TD_OK;
     }
     TD_HIP(ctx, hipSetDevice(ctx->device));
+    servers_quiesce(nullptr);
     if (n > ctx->mf_cap) {
         if (ctx->mf_dev) (void)hipFree(ctx->mf_dev);
         if (ctx->mf_host) (void)hipHostFree(ctx->mf_host);
@@ -457,6 +459,7 @@ int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const dou
         return set_err(ctx, TD_ERR_ARG, "td_evaluate: bad cell arrays");
     if (nCells > 0x7fffffff) return set_err(ctx, TD_ERR_ARG, "td_evaluate: too many cells");
     TD_HIP(ctx, hipSetDevice(ctx->device));
+    servers_quiesce((nearest_out || !ctx->incremental) ? nullptr : shadow_chain_of(ctx));
     int rc = (nearest_out || !ctx->incremental)
                  ? evaluate_full(ctx, xCell, yCell, zCell, zeta, nCells, ptS_out, phi_out, nearest_out)
                  : evaluate_incremental(ctx, xCell, yCell, zCell, zeta, nCells, ptS_out, phi_out);
@@ -476,6 +479,7 @@ int td_evaluate_batch(td_ctx *ctx, int64_t nmodels, const int64_t *cell_off, con
         if (b > a && (!xCell || !yCell || !zCell || !zeta))
             return set_err(ctx, TD_ERR_ARG, "td_evaluate_batch: bad cell arrays");
         TD_HIP(ctx, hipSetDevice(ctx->device));
+        servers_quiesce(nullptr);
         // independent models: the full evaluate (no shadow chain)
         int rc = evaluate_full(ctx, xCell + a, yCell + a, zCell + a, zeta + a, b - a,
                                ptS_out ? ptS_out + k * ctx->g.n : nullptr, phi_out ? phi_out + k : nullptr);
@@ -500,11 +504,13 @@ int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const 
     if (np == 0) return TD_OK;
     TD_HIP(ctx, hipSetDevice(ctx->device));
     if (np == 1 && !nearest_out && ctx->incremental && nCells > 0) {  // a chain's 1-point query (:81, :146)
+        servers_quiesce(shadow_chain_of(ctx));
         int handled = 0;
         int rc = interpolate_incremental(ctx, xCell, yCell, zCell, zeta, nCells, X[0], Y[0], Z[0], zeta_out, &handled);
         if (rc) return rc;
         if (handled) return TD_OK;
     }
+    servers_quiesce(nullptr);
     if (np > ctx->q_cap) {
         void *dev[] = {ctx->q, ctx->q_i, ctx->q_z};
         for (void *p : dev)
@@ -696,12 +702,15 @@ int tdt_nn_bench(td_ctx *ctx, const double *x, const double *y, const double *z,
     return TD_OK;
 }
 
-int tdt_set_incremental(td_ctx *ctx, int on) {
-    if (!ctx || on < 0 || on > 2) return TD_ERR_ARG;
-    if (on != ctx->incremental) shadow_free(ctx);
-    ctx->incremental = on;
+int td_set_incremental(td_ctx *ctx, int mode) {
+    if (!ctx) return set_err(nullptr, TD_ERR_ARG, "td_set_incremental: ctx is NULL");
+    if (mode < 0 || mode > 2) return set_err(ctx, TD_ERR_ARG, "td_set_incremental: mode must be 0, 1 or 2");
+    if (mode != ctx->incremental) shadow_free(ctx);
+    ctx->incremental = mode;
     return TD_OK;
 }
+
+int tdt_set_incremental(td_ctx *ctx, int on) { return td_set_incremental(ctx, on); }
 
 int tdt_set_nn_method(td_ctx *ctx, int method) {
     if (!ctx || method < 0 || method > 3) return TD_ERR_ARG;

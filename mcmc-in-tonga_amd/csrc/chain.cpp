@@ -18,6 +18,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tdstar_testing.h"
@@ -53,6 +54,20 @@ struct td_chain {
     hipStream_t srv_stream = nullptr;
     bool srv_running = false;
     std::chrono::steady_clock::time_point srv_last{};
+    ScriptStep srv_pending{};     // the step the server holds undecided (kDecideLater), if any
+    bool srv_has_pending = false;
+    td_rounds *rounds = nullptr;  // a resident tempering launch holds this chain (td_rounds_*)
+};
+
+// A resident tempering launch over chains of one context (chain_dev.h RoundBox).
+struct td_rounds {
+    std::vector<td_chain *> chains;
+    td_ctx *ctx = nullptr;
+    RoundBox *rb_host = nullptr, *rb_dev = nullptr;  // pinned, mapped
+    DevChain *desc_dev = nullptr, *desc_host = nullptr;
+    hipStream_t stream = nullptr;
+    bool running = false;
+    long long seq = 0;
 };
 
 namespace {
@@ -453,8 +468,36 @@ int device_pull_scalars(td_chain *ch) {
 
 int server_stop(td_chain *ch);
 
+// The resident servers this thread started.  A resident kernel occupies its
+// stream's hardware queue; HIP maps streams onto GPU_MAX_HW_QUEUES (4 on the
+// box) queues, so work on any other stream -- another context's, this
+// context's own, torch's, RCCL's -- may sit behind it until its watchdog.
+// servers_quiesce stops them before such work (include/tdstar.h, contexts).
+thread_local std::vector<td_chain *> t_servers;
+thread_local std::vector<td_rounds *> t_rounds;  // resident tempering launches of this thread
+int rounds_stop(td_rounds *r);
+
+}  // namespace
+
+namespace tdstar {
+void servers_quiesce(const td_chain *keep) {
+    const std::vector<td_chain *> run = t_servers;
+    for (td_chain *c : run)
+        if (c != keep) (void)server_stop(c);
+    const std::vector<td_rounds *> rr = t_rounds;
+    for (td_rounds *r : rr) (void)rounds_stop(r);
+}
+}  // namespace tdstar
+
+namespace {
+
 void free_chain(td_chain *ch) {
     if (!ch) return;
+    if (ch->rounds) (void)rounds_stop(ch->rounds);
+    if (ch->rounds) {  // the rounds object outlives the chain: forget it
+        auto &v = ch->rounds->chains;
+        v.erase(std::remove(v.begin(), v.end(), ch), v.end());
+    }
     (void)server_stop(ch);
     if (ch->srv_stream) (void)hipStreamDestroy(ch->srv_stream);
     if (ch->mb_host) (void)hipHostFree(ch->mb_host);
@@ -471,6 +514,11 @@ void free_chain(td_chain *ch) {
 //      mailbox in pinned host memory (chain_dev.h Mailbox) ----
 volatile long long *vol(long long *p) { return p; }
 
+// testing hook (tdt_set_server_post_delay): sleep between the alive check and the
+// post, so the kernel's idle watchdog fires first (the race of a descheduled host)
+std::atomic<int> g_post_delay_ms{0};
+constexpr int kExitedEarly = -1;  // server_post: the kernel returned before answering
+
 int server_stop(td_chain *ch) {
     if (!ch || !ch->srv_running) return TD_OK;
     Mailbox *m = ch->mb_host;
@@ -481,6 +529,8 @@ int server_stop(td_chain *ch) {
     }
     hipError_t e = hipStreamSynchronize(ch->srv_stream);  // the kernel returns (QUIT, or its idle watchdog)
     ch->srv_running = false;
+    ch->srv_has_pending = false;  // the kernel undid it
+    t_servers.erase(std::remove(t_servers.begin(), t_servers.end(), ch), t_servers.end());
     if (e != hipSuccess) return hip_err(ch->ctx, e, "chain server exit");
     adopt_scalars(ch);
     return TD_OK;
@@ -488,6 +538,7 @@ int server_stop(td_chain *ch) {
 
 int server_start(td_chain *ch) {
     if (ch->srv_running) return TD_OK;
+    servers_quiesce(ch);  // one resident kernel per thread
     td_ctx *c = ch->ctx;
     Mailbox *m = ch->mb_host;
     m->exited = 0;
@@ -506,10 +557,14 @@ int server_start(td_chain *ch) {
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (server)");
     ch->srv_running = true;
     ch->srv_last = std::chrono::steady_clock::now();
+    t_servers.push_back(ch);
     return TD_OK;
 }
 
 // Post the command already written into the mailbox and wait for its answer.
+// kExitedEarly: the kernel had returned (idle watchdog) before it read the
+// command -- its pending proposal undone, its state written back, nothing of
+// the command done; the caller re-issues it to a new launch.
 int server_post(td_chain *ch) {
     Mailbox *m = ch->mb_host;
     const long long sq = m->seq + 1;
@@ -519,9 +574,13 @@ int server_post(td_chain *ch) {
     for (long long spin = 0;; ++spin) {
         if (*vol(&m->done) == sq) break;
         if (*vol(&m->exited)) {  // returned before answering (it was idle past its watchdog)
-            (void)hipStreamSynchronize(ch->srv_stream);
+            const hipError_t e = hipStreamSynchronize(ch->srv_stream);
             ch->srv_running = false;
-            return set_err(ch->ctx, TD_ERR_HIP, "chain server returned before answering");
+            ch->srv_has_pending = false;
+            t_servers.erase(std::remove(t_servers.begin(), t_servers.end(), ch), t_servers.end());
+            if (e != hipSuccess) return hip_err(ch->ctx, e, "chain server exit");
+            adopt_scalars(ch);
+            return kExitedEarly;
         }
         if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20))
             return set_err(ch->ctx, TD_ERR_HIP, "chain server: no answer in 20 s");
@@ -531,9 +590,160 @@ int server_post(td_chain *ch) {
     return TD_OK;
 }
 
+// ---- resident tempering rounds ----
+int rounds_stop(td_rounds *r) {
+    if (!r || !r->running) return TD_OK;
+    RoundBox *b = r->rb_host;
+    b->cmd = kRoundQuit;
+    b->K = 0;
+    std::atomic_thread_fence(std::memory_order_release);
+    *vol(&b->seq) = ++r->seq;
+    const hipError_t e = hipStreamSynchronize(r->stream);  // every workgroup returns (QUIT or its watchdog)
+    r->running = false;
+    t_rounds.erase(std::remove(t_rounds.begin(), t_rounds.end(), r), t_rounds.end());
+    if (e != hipSuccess) return hip_err(r->ctx, e, "tempering rounds exit");
+    for (td_chain *ch : r->chains) adopt_scalars(ch);
+    return TD_OK;
+}
+
+int rounds_start(td_rounds *r) {
+    if (r->running) return TD_OK;
+    td_ctx *c = r->ctx;
+    servers_quiesce(nullptr);  // (stops every other resident launch of this thread)
+    RoundBox *b = r->rb_host;
+    const int nc = (int)r->chains.size();
+    for (int k = 0; k < nc; ++k) {
+        b->slot[k].done = r->seq;  // the workgroup waits for a seq past this
+        b->slot[k].exited = 0;
+        r->desc_host[k] = r->chains[(size_t)k]->dev;
+        r->chains[(size_t)k]->desc_dirty = true;  // (its own descriptor copy is refreshed on its next run)
+    }
+    b->seq = r->seq;
+    std::atomic_thread_fence(std::memory_order_release);
+    hipError_t e = hipMemcpyAsync(r->desc_dev, r->desc_host, sizeof(DevChain) * (size_t)nc, hipMemcpyHostToDevice,
+                                  r->stream);
+    if (e != hipSuccess) return hip_err(c, e, "tempering rounds descriptors");
+    ScriptArgs sa{};
+    sa.rb = r->rb_dev;
+    e = chain_run(r->desc_host, r->desc_dev, nc, LLONG_MAX, r->stream, &sa);
+    if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (tempering rounds)");
+    r->running = true;
+    t_rounds.push_back(r);
+    return TD_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int td_rounds_create(td_rounds **out, td_chain *const *chains, int64_t nchains) {
+    if (!out || !chains || nchains <= 0 || nchains > 65536) return set_err(nullptr, TD_ERR_ARG, "td_rounds_create");
+    *out = nullptr;
+    td_ctx *c = chains[0] ? chains[0]->ctx : nullptr;
+    if (!c) return set_err(nullptr, TD_ERR_ARG, "td_rounds_create: NULL chain");
+    for (int64_t b = 0; b < nchains; ++b) {
+        if (!chains[b] || chains[b]->ctx != c || chains[b]->engine != TD_ENGINE_DEVICE || chains[b]->rounds)
+            return set_err(c, TD_ERR_ARG, "td_rounds_create: DEVICE chains of one context, each in one td_rounds");
+        for (int64_t k = 0; k < b; ++k)
+            if (chains[k] == chains[b]) return set_err(c, TD_ERR_ARG, "td_rounds_create: a chain appears twice");
+    }
+    // every workgroup must be resident at once (each waits for the host between rounds): one per CU
+    if (nchains > c->num_cus)
+        return set_err(c, TD_ERR_ARG, "td_rounds_create: more chains than compute units (one resident workgroup each)");
+    td_rounds *r = new (std::nothrow) td_rounds();
+    if (!r) return set_err(c, TD_ERR_NOMEM, "td_rounds_create");
+    r->ctx = c;
+    r->chains.assign(chains, chains + nchains);
+    const size_t bytes = sizeof(RoundBox) + sizeof(RoundSlot) * (size_t)nchains;
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipHostMalloc(&r->rb_host, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+        std::memset(r->rb_host, 0, bytes);
+        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&r->rb_dev), r->rb_host, 0);
+    }
+    if (e == hipSuccess) e = hipMalloc(&r->desc_dev, sizeof(DevChain) * (size_t)nchains);
+    if (e == hipSuccess) e = hipHostMalloc(&r->desc_host, sizeof(DevChain) * (size_t)nchains, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        (void)td_rounds_destroy(r);
+        return hip_err(c, e, "td_rounds_create");
+    }
+    for (td_chain *ch : r->chains) ch->rounds = r;
+    *out = r;
+    return TD_OK;
+}
+
+int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out) {
+    if (!r || K <= 0 || K > INT32_MAX || !temps) return set_err(r ? r->ctx : nullptr, TD_ERR_ARG, "td_rounds_run");
+    const int nc = (int)r->chains.size();
+    if (nc == 0) return set_err(r->ctx, TD_ERR_ARG, "td_rounds_run: its chains were destroyed");
+    for (int k = 0; k < nc; ++k)
+        if (!(temps[k] > 0.0)) return set_err(r->ctx, TD_ERR_ARG, "td_rounds_run: need T > 0");
+    TD_HIP(r->ctx, hipSetDevice(r->ctx->device));
+    for (int attempt = 0;; ++attempt) {
+        int rc = rounds_start(r);
+        if (rc) return rc;
+        RoundBox *b = r->rb_host;
+        for (int k = 0; k < nc; ++k) {  // the chain's temperature: its host params too (td_chain_set_temperature)
+            td_chain *ch = r->chains[(size_t)k];
+            ch->prm.temperature = temps[k];
+            ch->P.temperature = temps[k];
+            tdchain::params_derived(ch->P);
+            ch->dev.params = ch->P;
+            b->slot[k].T = ch->P.temperature;
+            b->slot[k].inv_2t = ch->P.inv_2t;
+        }
+        b->cmd = kRoundRun;
+        b->K = (int)K;
+        std::atomic_thread_fence(std::memory_order_release);
+        const long long sq = ++r->seq;
+        *vol(&b->seq) = sq;
+        bool lost = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < nc && !lost; ++k)
+            for (long long spin = 0;; ++spin) {
+                if (*vol(&b->slot[k].done) == sq) break;
+                if (*vol(&b->slot[k].exited)) {  // its watchdog fired before this round was posted
+                    lost = true;
+                    break;
+                }
+                if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+                    return set_err(r->ctx, TD_ERR_HIP, "tempering rounds: no answer in 60 s");
+            }
+        if (!lost) break;
+        // the launch returned between rounds (state consistent, nothing of this round run):
+        // collect it and post the round again to a new launch
+        const hipError_t e = hipStreamSynchronize(r->stream);
+        r->running = false;
+        t_rounds.erase(std::remove(t_rounds.begin(), t_rounds.end(), r), t_rounds.end());
+        if (e != hipSuccess) return hip_err(r->ctx, e, "tempering rounds exit");
+        for (td_chain *ch : r->chains) adopt_scalars(ch);
+        --r->seq;  // this seq was never run
+        if (attempt > 2) return set_err(r->ctx, TD_ERR_HIP, "tempering rounds: the launch keeps returning");
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    for (int k = 0; k < nc; ++k) {
+        td_chain *ch = r->chains[(size_t)k];
+        const double phi = *reinterpret_cast<volatile double *>(&r->rb_host->slot[k].phi);
+        ch->phi = phi;
+        ch->stats.phi = phi;
+        ch->stats.iterations += K;
+        if (phi_out) phi_out[k] = phi;
+    }
+    return TD_OK;
+}
+
+int td_rounds_destroy(td_rounds *r) {
+    if (!r) return TD_OK;
+    int rc = rounds_stop(r);
+    for (td_chain *ch : r->chains) ch->rounds = nullptr;
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    if (r->rb_host) (void)hipHostFree(r->rb_host);
+    if (r->desc_dev) (void)hipFree(r->desc_dev);
+    if (r->desc_host) (void)hipHostFree(r->desc_host);
+    delete r;
+    return rc;
+}
 
 int td_chain_create(td_chain **out, td_ctx *ctx, const td_chain_params *params, const double *xCell,
                     const double *yCell, const double *zCell, const double *zeta, int64_t nCells) {
@@ -552,6 +762,7 @@ int td_chain_create(td_chain **out, td_ctx *ctx, const td_chain_params *params, 
         return set_err(ctx, TD_ERR_ARG, "td_chain_create: bad cell arrays");
     td_chain *ch = new (std::nothrow) td_chain();
     if (!ch) return set_err(ctx, TD_ERR_NOMEM, "td_chain_create: out of memory");
+    servers_quiesce(nullptr);
     ch->ctx = ctx;
     ch->prm = p;
     ch->P = make_params(p);
@@ -601,6 +812,7 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
     if (iterations == 0) return TD_OK;
     hipError_t e = hipSetDevice(ch->ctx->device);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "hipSetDevice");
+    if (ch->engine != TD_ENGINE_DROPIN) servers_quiesce(nullptr);  // DROPIN's td_evaluate keeps its own
     if (ch->engine != TD_ENGINE_DEVICE) {
         for (int64_t i = 0; i < iterations; ++i) {
             int rc = host_iteration(ch);
@@ -640,6 +852,7 @@ int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterati
             if (chains[k] == chains[b]) return set_err(c, TD_ERR_ARG, "td_chain_run_batch: a chain appears twice");
     }
     if (iterations == 0) return TD_OK;
+    if (!host) servers_quiesce(nullptr);
     if (host || nchains == 1) {  // the host engine is the sequential parity twin
         for (int64_t b = 0; b < nchains; ++b) {
             int rc = td_chain_run(chains[b], iterations);
@@ -678,6 +891,10 @@ int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterati
 
 int td_chain_stats_get(const td_chain *ch, td_chain_stats *st) {
     if (!ch || !st) return TD_ERR_ARG;
+    if (ch->rounds && ch->rounds->running) {  // the counts are the launch's until it returns
+        int rc = rounds_stop(ch->rounds);
+        if (rc) return rc;
+    }
     *st = ch->stats;
     return TD_OK;
 }
@@ -688,6 +905,7 @@ int td_chain_get_model(const td_chain *chc, double *xCell, double *yCell, double
     if (!ch) return TD_ERR_ARG;
     td_ctx *c = ch->ctx;
     if (ch->engine == TD_ENGINE_DEVICE) {
+        servers_quiesce(nullptr);
         int rc = device_pull_scalars(ch);
         if (rc) return rc;
         const int N = ch->st_host->ncells, cp = ch->dev.cap;
@@ -856,15 +1074,41 @@ bool shadow_server_alive(td_chain *ch) {
 int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,
                        double *phi_out, double *ptS_out) {
     if (nsteps < 1 || nsteps > kMaxScript) return set_err(ch->ctx, TD_ERR_ARG, "server steps");
-    int rc = server_start(ch);
-    if (rc) return rc;
-    Mailbox *m = ch->mb_host;
-    m->type = kCmdEval;
-    m->decision = decision;
-    m->nsteps = nsteps;
-    for (int k = 0; k < nsteps; ++k) m->step[k] = steps[k];
-    rc = server_post(ch);
-    if (rc) return rc;
+    ScriptStep st[kMaxScript];
+    for (int k = 0; k < nsteps; ++k) st[k] = steps[k];
+    for (int attempt = 0;; ++attempt) {
+        int rc = server_start(ch);
+        if (rc) return rc;
+        if (attempt == 0 && g_post_delay_ms.load() > 0)
+            std::this_thread::sleep_for(std::chrono::milliseconds(g_post_delay_ms.load()));
+        Mailbox *m = ch->mb_host;
+        m->type = kCmdEval;
+        m->decision = decision;
+        m->nsteps = nsteps;
+        for (int k = 0; k < nsteps; ++k) m->step[k] = st[k];
+        const ScriptStep held = ch->srv_pending;
+        const bool had = ch->srv_has_pending;
+        rc = server_post(ch);
+        if (rc == TD_OK) {
+            ch->srv_pending = st[nsteps - 1];
+            ch->srv_has_pending = st[nsteps - 1].decision == kDecideLater;
+            break;
+        }
+        if (rc != kExitedEarly || attempt > 0) {
+            return rc == kExitedEarly ? set_err(ch->ctx, TD_ERR_HIP, "chain server returned before answering twice")
+                                      : rc;
+        }
+        // the kernel undid its pending proposal and never read this command: a fresh launch
+        // gets it again, preceded by that proposal as a committed step if the caller accepted it
+        if (decision == 1 && had) {
+            if (nsteps + 1 > kMaxScript) return set_err(ch->ctx, TD_ERR_HIP, "chain server: lost a pending commit");
+            for (int k = nsteps; k > 0; --k) st[k] = st[k - 1];
+            st[0] = held;
+            st[0].decision = 1;
+            ++nsteps;
+        }
+        decision = 0;  // nothing pending on the new launch
+    }
     unpack_report(ch->script_host, ch->ctx->g.n, base_ptS, phi_out, ptS_out);
     return TD_OK;
 }
@@ -872,6 +1116,7 @@ int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int 
 int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val) {
     int rc = server_start(ch);
     if (rc) return rc;
+    if (g_post_delay_ms.load() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(g_post_delay_ms.load()));
     Mailbox *m = ch->mb_host;
     m->type = kCmdQuery;
     m->q[0] = x;
@@ -880,6 +1125,9 @@ int shadow_server_query(td_chain *ch, double x, double y, double z, const Script
     m->has_edit = edit ? 1 : 0;
     if (edit) m->qedit = *edit;
     rc = server_post(ch);
+    // the kernel had returned (its pending proposal undone: the caller sees the server
+    // stopped and re-issues that proposal's commit): answer with a one-off launch
+    if (rc == kExitedEarly) return shadow_chain_query(ch, x, y, z, edit, val);
     if (rc) return rc;
     *val = m->qval;
     return TD_OK;
@@ -928,6 +1176,11 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
     const double v[8] = {(double)p.action, (double)p.active, (double)p.valid, (double)p.index, p.x, p.y, p.z, p.zeta};
     std::memcpy(out, v, sizeof v);
     return 0;
+}
+int tdt_set_server_post_delay(int ms) {
+    if (ms < 0) return TD_ERR_ARG;
+    g_post_delay_ms.store(ms);
+    return TD_OK;
 }
 int tdt_chain_set_lds_mode(td_chain *ch, int mode) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE || mode < 0 || mode > 1) return TD_ERR_ARG;

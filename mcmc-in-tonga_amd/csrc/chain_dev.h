@@ -145,12 +145,35 @@ struct Mailbox {
     long long diag[4];  // diagnostic: shader cycles and 100 MHz ticks of the last busy interval, polls
 };
 
+// Resident tempering rounds (td_rounds_*, chain.cpp): a td_chain_run_batch
+// launch that stays resident across swap rounds.  Every K proposals each
+// workgroup publishes its chain's phi and waits for the next round's
+// temperature (parallel tempering, SURVEY 8e: the host gathers the phis,
+// decides the swaps and posts the new temperatures) -- no launch per round.
+// Pinned host memory; one 64-B slot per chain.
+enum RoundCmd : int { kRoundRun = 1, kRoundQuit = 3 };
+struct RoundSlot {
+    double T, inv_2t;  // host -> device: the chain's temperature for the round (inv_2t = 1/(2T), host-computed)
+    long long done;    // device -> host: seq of the last round finished
+    double phi;        // the chain's phi after that round
+    long long exited;  // the workgroup returned (QUIT, or its idle watchdog at a round boundary)
+    long long pad[3];
+};
+struct RoundBox {
+    long long seq;  // host -> device (written last)
+    int cmd;        // RoundCmd
+    int K;          // proposals in the round
+    long long pad[6];
+    RoundSlot slot[1];  // [nchains]
+};
+
 struct ScriptArgs {
     int n;
     int pin;  // >= 0: the chain runs on the workgroup that lands on this XCD (L2 kept warm across launches)
     ScriptStep step[kMaxScript];
     double *out;
-    Mailbox *mb;  // server mode (device address of pinned host memory)
+    Mailbox *mb;   // server mode (device address of pinned host memory)
+    RoundBox *rb;  // resident tempering rounds (device address of pinned host memory), free-running chains
 };
 
 // Build the cache from scratch for the cells currently in slots 0..ncells-1
@@ -186,6 +209,9 @@ int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int 
                        double *phi_out, double *ptS_out);
 int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val);
 int shadow_server_stop(td_chain *ch);
+// Stop every resident server this thread runs except `keep` (nullable): called
+// before work on any other stream (chain.cpp t_servers).
+void servers_quiesce(const td_chain *keep);
 void shadow_server_diag(const td_chain *ch, int64_t out[4]);
 int shadow_profile(td_chain *ch, int64_t out[80]);
 // One-point Interpolation against the chain's model (edit == NULL) or that

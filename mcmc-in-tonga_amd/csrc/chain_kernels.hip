@@ -187,6 +187,10 @@ struct Shared {
     ScriptStep step_cur;
     ScriptStep srv_step[kMaxScript];
     int srv_n, srv_k, srv_quit;
+    // resident tempering rounds: the temperature of the current round (for reject_bound) and its last seq
+    double rT, rinv2t;
+    long long rseq;
+    int rK;
     long long srv_seq, srv_busy_c, srv_busy_w;
     long long mbox[32];  // server mode: the last command read from the mailbox
     OrphanRec orph[kOrphanLds];
@@ -659,6 +663,49 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
     }
 }
 
+// Resident tempering rounds, wave 0 at a round boundary: publish the chain's
+// phi for the round just finished (done = its seq), then wait for the next
+// command: RUN (K proposals at the slot's new temperature) or QUIT; silence
+// past the idle watchdog is a QUIT (the state is consistent between rounds).
+// Results in sh.rK / sh.rT / sh.rinv2t / sh.srv_quit.
+__device__ void round_wait(RoundBox *rb, int b, Shared &sh, int lane, bool publish, double phi) {
+    RoundSlot *slot = &rb->slot[b];
+    if (publish && lane == 0) {
+        mb_store(reinterpret_cast<long long *>(&slot->phi), __double_as_longlong(phi));
+        __threadfence_system();
+        mb_store(&slot->done, sh.rseq);
+    }
+    const long long seen = sh.rseq;
+    long long t0 = (long long)wall_clock64();
+    while (true) {
+        const long long sq = mb_load(&rb->seq);
+        if (sq != seen) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            if (lane == 0) {
+                const long long w = mb_load(reinterpret_cast<const long long *>(rb) + 1);  // cmd | K << 32
+                const int cmd = (int)(w & 0xffffffffll), K = (int)(w >> 32);
+                sh.rseq = sq;
+                if (cmd == kRoundRun && K > 0) {
+                    sh.rK = K;
+                    sh.rT = __longlong_as_double(mb_load(reinterpret_cast<const long long *>(&slot->T)));
+                    sh.rinv2t = __longlong_as_double(mb_load(reinterpret_cast<const long long *>(&slot->inv_2t)));
+                    sh.srv_quit = 0;
+                } else {
+                    sh.srv_quit = 1;
+                }
+            }
+            wave_sync_lds();
+            return;
+        }
+        if ((long long)wall_clock64() - t0 > kServerIdleTicks) {
+            if (lane == 0) sh.srv_quit = 1;
+            wave_sync_lds();
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 // One array of a fused block copy: U elements per thread per round, loaded
 // into registers by load(), written by store().  Several Segs loaded before
 // any is stored keep all their loads in flight at once: the launch preamble
@@ -705,6 +752,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const bool prof_on = d.profile != 0;
     const long long t_start = prof_on ? clock64() : 0;  // diagnostic: launch preamble / epilogue (prof[76..79])
     Mailbox *const mb = SCRIPT ? sa.mb : nullptr;  // server mode: resident, steps from the mailbox (iters ignored)
+    RoundBox *const rbx = SCRIPT ? nullptr : sa.rb;  // resident tempering rounds (iters ignored)
+    const int bchain = sa.pin >= 0 ? 0 : (int)blockIdx.x;
     const int nscript = SCRIPT ? (mb ? 1 : sa.n) : 0;  // > 0: host-given proposals (td_evaluate), iters == nscript
 
     // ---- views: LDS copies of the tile / ray / order arrays when they fit ----
@@ -786,6 +835,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.nfree = s0.nfree;
         sh.g_op = 0;
         sh.grid_ovf = *d.grid_overflow;
+        sh.rT = P.temperature;
+        sh.rinv2t = P.inv_2t;
+        sh.srv_quit = 0;
+        sh.rK = 0;
         for (int k = 0; k < kProfSlots; ++k) sh.prof[k] = 0;
         sh.t_last = clock64();
         sh.dseg.nseg = 0;
@@ -834,7 +887,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             wave_sync_lds();
             server_wait(mb, d, v, sh, lane);
         }
-        if (lane == 0 && iters > 0 && !(mb && sh.srv_quit)) {
+        if (rbx) {  // the first round (the last one done is in the slot)
+            if (lane == 0) sh.rseq = mb_load(&rbx->slot[bchain].done);
+            wave_sync_lds();
+            round_wait(rbx, bchain, sh, lane, false, 0.0);
+        }
+        if (lane == 0 && iters > 0 && !((mb || rbx) && sh.srv_quit)) {
             if (nscript) {
                 sh.step_cur = mb ? sh.srv_step[sh.srv_k++] : sa.step[0];
                 script_proposal(sh.ps[0], sh.step_cur, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz, d.czeta,
@@ -866,12 +924,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         }
     }
     double phi_r = sh.phi;
+    // wave 0: the temperature of the round (tid 0 decides with it) and the round's last iteration
+    double inv2t_r = sh.rinv2t;
+    long long round_end = rbx ? sh.rK : LLONG_MAX;
     int cur_r = 0;
     bool pend_r = false;    // rays in HBM: an accepted proposal's chi^2 partial sums not yet written
     bool pend_sup = false;  // rays in HBM: its super-tiles' maxima not yet refreshed
     int last_action = 0, last_accept = 0;  // tid 0: Model.action / accept of the last iteration
     long long it_done = 0;                 // iterations run (server mode: until QUIT)
-    for (long long it = 0; it < iters && !(mb && sh.srv_quit); ++it) {
+    for (long long it = 0; it < iters && !((mb || rbx) && sh.srv_quit); ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
         // rays in HBM: the previous accepted proposal's super-tile maxima (their first round of
         // loads issued here, so it overlaps the partial sums' commit below)
@@ -1275,8 +1336,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // a scripted step's decision is given (kDecideLater: by the server's next command;
                 // the grid update below is then staged and applied only if it is a commit)
                 const bool acc = nscript ? sh.step_cur.decision == 1
-                                         : !early && tdchain::accept(P, pp, phi_r, phi_n, czeta, zeta_killed,
-                                                                     zetanew_death, sh.lnN);
+                                         : !early && tdchain::accept_t(P, inv2t_r, pp, phi_r, phi_n, czeta,
+                                                                       zeta_killed, zetanew_death, sh.lnN);
                 acc_r = acc;
                 sh.accept = acc ? 1 : 0;
                 sh.phi_n = phi_n;
@@ -1335,7 +1396,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 const int k0 = sh.k0;
                 if (!WALK && fwd && k0 < n && !nscript) {
                     // the bound first: it does not depend on the sum (computed while the terms load)
-                    const double thr = tdchain::reject_bound(P, pp, sh.phi, czeta, zeta_killed, zetanew_death, sh.lnN);
+                    const double thr = tdchain::reject_bound_t(P, sh.rT, sh.rinv2t, pp, sh.phi, czeta, zeta_killed,
+                                                               zetanew_death, sh.lnN);
                     const double C0 = k0 > 0 ? v.prefix[k0 - 1] : 0.0;
                     double part = 0.0;
                     for (int k = k0 + lane; k < n; k += 64) part = part + v.term[k];
@@ -1498,7 +1560,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         // ===== end of iteration: the next proposal (wave 0; draws refilled every 64) =====
         if (wv == 0) {
             if (prof_on && lane == 0) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
-            if (it + 1 < iters && !(mb && sh.srv_quit)) {
+            if (rbx && it + 1 == round_end) {  // a tempering round is done: publish phi, take the next temperature
+                round_wait(rbx, bchain, sh, lane, true, phi_r);  // (lane 0 = tid 0 holds phi)
+                inv2t_r = sh.rinv2t;
+                round_end = it + 1 + sh.rK;
+            }
+            if (it + 1 < iters && !((mb || rbx) && sh.srv_quit)) {
                 if (((it + 1) & 63) == 0 && !nscript) {
                     wave_sync_lds();
                     draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(iter0 + it + 1 + lane));
@@ -1588,6 +1655,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         if (mb) {
             __threadfence_system();
             mb_store(&mb->exited, 1);
+        }
+        if (rbx) {
+            __threadfence_system();
+            mb_store(&rbx->slot[bchain].exited, 1);
         }
     }
 }

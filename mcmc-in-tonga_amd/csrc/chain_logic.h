@@ -343,10 +343,12 @@ inline void log_window(double out[3], int64_t N) {
 // Written as one if-chain into one variable: a `switch` with a `return -x`
 // default was miscompiled for gfx950 (the default path returned a stale
 // register; tools/repro_accept.hip).
-TD_HD double log_alpha(const Params &P, const Proposal &p, double phi, double phi_n, double czeta,
-                       double zeta_killed, double zetanew_death, const double *lnN) {
+// inv_2t = 1/(2T) of the chain's current temperature (P.inv_2t; a resident
+// tempering launch keeps its own, set between rounds)
+TD_HD double log_alpha_t(const Params &P, double inv_2t, const Proposal &p, double phi, double phi_n, double czeta,
+                         double zeta_killed, double zetanew_death, const double *lnN) {
     // (multiplications by precomputed reciprocals: no division on the device's decision path)
-    const double g = (phi - phi_n) * P.inv_2t;
+    const double g = (phi - phi_n) * inv_2t;
     double la = g;
     if (p.action == kBirth) {
         const double dz = czeta - p.zeta;
@@ -366,12 +368,20 @@ TD_HD double log_alpha(const Params &P, const Proposal &p, double phi, double ph
     }
     return la;
 }
-TD_HD bool accept(const Params &P, const Proposal &p, double phi, double phi_n, double czeta, double zeta_killed,
-                  double zetanew_death, const double *lnN) {
+TD_HD double log_alpha(const Params &P, const Proposal &p, double phi, double phi_n, double czeta,
+                       double zeta_killed, double zetanew_death, const double *lnN) {
+    return log_alpha_t(P, P.inv_2t, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN);
+}
+TD_HD bool accept_t(const Params &P, double inv_2t, const Proposal &p, double phi, double phi_n, double czeta,
+                    double zeta_killed, double zetanew_death, const double *lnN) {
     if (!p.active || !p.valid) return false;  // rand(1)[1] < alpha && valid == 1
     // exponential death: valid only when the reduced model's value at the killed site is > 0 (:165, :171)
     if (p.action == kDeath && P.prior == kExponential && !(zetanew_death > 0.0)) return false;
-    return p.log_u < log_alpha(P, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN);
+    return p.log_u < log_alpha_t(P, inv_2t, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN);
+}
+TD_HD bool accept(const Params &P, const Proposal &p, double phi, double phi_n, double czeta, double zeta_killed,
+                  double zetanew_death, const double *lnN) {
+    return accept_t(P, P.inv_2t, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN);
 }
 
 // The phi_n from which accept() rejects: log_alpha is dphi-affine, so
@@ -380,11 +390,15 @@ TD_HD bool accept(const Params &P, const Proposal &p, double phi, double phi_n, 
 // chi^2 partial sums only grow); the caller adds a margin far above every
 // rounding involved, so the outcome is the one accept() gives on the exact
 // phi_n.  +inf when no finite bound exists (u == 0).
+TD_HD double reject_bound_t(const Params &P, double temperature, double inv_2t, const Proposal &p, double phi,
+                            double czeta, double zeta_killed, double zetanew_death, const double *lnN) {
+    if (!(p.u_accept > 0.0)) return __builtin_huge_val();
+    const double lf = log_alpha_t(P, inv_2t, p, phi, phi, czeta, zeta_killed, zetanew_death, lnN);  // dphi = 0
+    return phi + 2.0 * temperature * (lf - p.log_u);  // (a bound: its own rounding is covered by the margin)
+}
 TD_HD double reject_bound(const Params &P, const Proposal &p, double phi, double czeta, double zeta_killed,
                           double zetanew_death, const double *lnN) {
-    if (!(p.u_accept > 0.0)) return __builtin_huge_val();
-    const double lf = log_alpha(P, p, phi, phi, czeta, zeta_killed, zetanew_death, lnN);  // dphi = 0
-    return phi + 2.0 * P.temperature * (lf - p.log_u);  // (a bound: its own rounding is covered by the margin)
+    return reject_bound_t(P, P.temperature, P.inv_2t, p, phi, czeta, zeta_killed, zetanew_death, lnN);
 }
 
 }  // namespace tdchain

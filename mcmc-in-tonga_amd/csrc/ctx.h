@@ -111,6 +111,10 @@ int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z
 int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                          int64_t ncells, double *ptS_out, double *phi_out);
 void shadow_free(td_ctx *ctx);
+// The shadow chain of td_evaluate's incremental path (nullptr if none).
+td_chain *shadow_chain_of(td_ctx *ctx);
+// Stop every resident server this thread runs except `keep` (chain.cpp).
+void servers_quiesce(const td_chain *keep);
 // td_interpolate of one point on the shadow's model (incremental.cpp); *handled = 0: not applicable.
 int interpolate_incremental(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                             int64_t ncells, double qx, double qy, double qz, double *val, int *handled);

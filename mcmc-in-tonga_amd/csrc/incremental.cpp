@@ -268,6 +268,8 @@ int build_shadow(td_ctx *ctx, td_shadow *s) {
 
 }  // namespace
 
+td_chain *shadow_chain_of(td_ctx *ctx) { return ctx->shadow ? ctx->shadow->ch : nullptr; }
+
 void shadow_free(td_ctx *ctx) {
     if (!ctx->shadow) return;
     drop_chain(ctx->shadow);

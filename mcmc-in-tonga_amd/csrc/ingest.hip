@@ -36,14 +36,27 @@ __device__ __forceinline__ int knot_interval(const double *__restrict__ k, int n
     return lo < n - 1 ? lo : n - 2;
 }
 
-__global__ __launch_bounds__(256) void k_trilinear(const double *__restrict__ xs, int nx,
-                                                   const double *__restrict__ ys, int ny,
-                                                   const double *__restrict__ zs, int nz,
-                                                   const double *__restrict__ v, const double *__restrict__ px,
-                                                   const double *__restrict__ py, const double *__restrict__ pz,
-                                                   int npts, double *__restrict__ out,
-                                                   unsigned long long *__restrict__ outside) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// Knots (nx + ny + nz doubles) are staged in LDS when they fit: the three
+// binary searches are chains of dependent loads, LDS round trips instead of L2.
+constexpr int kTriThreads = 256;
+constexpr int kKnotsLds = 4096;  // 32 KB
+
+__global__ __launch_bounds__(kTriThreads) void k_trilinear(const double *__restrict__ knots, int nx, int ny, int nz,
+                                                           const double *__restrict__ v,
+                                                           const double *__restrict__ px,
+                                                           const double *__restrict__ py,
+                                                           const double *__restrict__ pz, int npts,
+                                                           double *__restrict__ out,
+                                                           unsigned long long *__restrict__ outside) {
+    __shared__ double kl[kKnotsLds];
+    const int ng = nx + ny + nz;
+    const bool lds = ng <= kKnotsLds;
+    if (lds)
+        for (int i = threadIdx.x; i < ng; i += kTriThreads) kl[i] = knots[i];
+    __syncthreads();
+    const double *k0 = lds ? kl : knots;
+    const double *xs = k0, *ys = k0 + nx, *zs = k0 + nx + ny;
+    const int p = blockIdx.x * kTriThreads + threadIdx.x;
     if (p >= npts) return;
     const double x = px[p], y = py[p], z = pz[p];
     const int i = knot_interval(xs, nx, x), j = knot_interval(ys, ny, y), k = knot_interval(zs, nz, z);
@@ -56,16 +69,35 @@ __global__ __launch_bounds__(256) void k_trilinear(const double *__restrict__ xs
     const double ty = (y - ys[j]) / (ys[j + 1] - ys[j]);
     const double tz = (z - zs[k]) / (zs[k + 1] - zs[k]);
     const double ux = 1.0 - tx, uy = 1.0 - ty, uz = 1.0 - tz;
-    // column-major [nx][ny][nz] (Julia's sn[1, :, :, :]): x fastest
+    // column-major [nx][ny][nz] (Julia's sn[1, :, :, :]): x fastest; the 8 corners loaded at once
     auto at = [&](int a, int b, int c) { return v[((long)c * ny + b) * nx + a]; };
+    double cv[2][2][2];
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) cv[dz][dy][dx] = at(i + dx, j + dy, k + dz);
     double c2[2];
+#pragma unroll
     for (int dz = 0; dz < 2; ++dz) {
         double c1[2];
-        for (int dy = 0; dy < 2; ++dy) c1[dy] = ux * at(i, j + dy, k + dz) + tx * at(i + 1, j + dy, k + dz);
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) c1[dy] = ux * cv[dz][dy][0] + tx * cv[dz][dy][1];
         c2[dz] = uy * c1[0] + ty * c1[1];
     }
     out[p] = uz * c2[0] + tz * c2[1];
 }
+
+// Device buffers and a stream kept across calls, per thread and device (the
+// call is context-free): no hipMalloc / hipFree per call.
+struct TriCache {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    void *buf = nullptr;
+    size_t cap = 0;
+};
+thread_local TriCache t_tri;
 
 }  // namespace
 
@@ -90,30 +122,49 @@ extern "C" int td_trilinear(int device, const double *xs, int64_t nx, const doub
     *n_outside = 0;
     if (npts == 0) return TD_OK;
     if (hipSetDevice(device) != hipSuccess) return set_err(nullptr, TD_ERR_HIP, "td_trilinear: hipSetDevice");
+    servers_quiesce(nullptr);
+    TriCache &c = t_tri;
+    hipError_t e = hipSuccess;
+    if (c.device != device) {
+        if (c.device >= 0) {  // another device: the old one's buffers go
+            (void)hipSetDevice(c.device);
+            if (c.buf) (void)hipFree(c.buf);
+            if (c.stream) (void)hipStreamDestroy(c.stream);
+            (void)hipSetDevice(device);
+        }
+        c = TriCache{};
+        e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return set_err(nullptr, TD_ERR_HIP, "td_trilinear: hipStreamCreate");
+        c.device = device;
+    }
     const size_t ng = (size_t)(nx + ny + nz), nv = (size_t)(nx * ny * nz), np = (size_t)npts;
-    void *buf = nullptr;
     const size_t bytes = sizeof(double) * (ng + nv + 4 * np) + sizeof(unsigned long long);
-    if (hipMalloc(&buf, bytes) != hipSuccess) return set_err(nullptr, TD_ERR_NOMEM, "td_trilinear: hipMalloc");
-    double *dg = static_cast<double *>(buf), *dv = dg + ng, *dp = dv + nv, *dout = dp + 3 * np;
+    if (bytes > c.cap) {
+        if (c.buf) (void)hipFree(c.buf);
+        c.buf = nullptr;
+        c.cap = 0;
+        if (hipMalloc(&c.buf, bytes + bytes / 4) != hipSuccess)
+            return set_err(nullptr, TD_ERR_NOMEM, "td_trilinear: hipMalloc");
+        c.cap = bytes + bytes / 4;
+    }
+    double *dg = static_cast<double *>(c.buf), *dv = dg + ng, *dp = dv + nv, *dout = dp + 3 * np;
     auto *dcnt = reinterpret_cast<unsigned long long *>(dout + np);
-    hipError_t e = hipMemcpy(dg, xs, sizeof(double) * nx, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dg + nx, ys, sizeof(double) * ny, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dg + nx + ny, zs, sizeof(double) * nz, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dv, values, sizeof(double) * nv, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dp, px, sizeof(double) * np, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dp + np, py, sizeof(double) * np, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dp + 2 * np, pz, sizeof(double) * np, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(dcnt, 0, sizeof(unsigned long long));
+    const struct { void *d; const void *h; size_t b; } up[] = {
+        {dg, xs, sizeof(double) * nx}, {dg + nx, ys, sizeof(double) * ny}, {dg + nx + ny, zs, sizeof(double) * nz},
+        {dv, values, sizeof(double) * nv}, {dp, px, sizeof(double) * np}, {dp + np, py, sizeof(double) * np},
+        {dp + 2 * np, pz, sizeof(double) * np}};
+    for (const auto &u : up)
+        if (e == hipSuccess) e = hipMemcpyAsync(u.d, u.h, u.b, hipMemcpyHostToDevice, c.stream);
+    if (e == hipSuccess) e = hipMemsetAsync(dcnt, 0, sizeof(unsigned long long), c.stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_trilinear, dim3((unsigned)((npts + 255) / 256)), dim3(256), 0, nullptr, dg, (int)nx,
-                           dg + nx, (int)ny, dg + nx + ny, (int)nz, dv, dp, dp + np, dp + 2 * np, (int)npts, dout,
-                           dcnt);
+        hipLaunchKernelGGL(k_trilinear, dim3((unsigned)((npts + kTriThreads - 1) / kTriThreads)), dim3(kTriThreads), 0,
+                           c.stream, dg, (int)nx, (int)ny, (int)nz, dv, dp, dp + np, dp + 2 * np, (int)npts, dout, dcnt);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(double) * np, hipMemcpyDeviceToHost);
     unsigned long long cnt = 0;
-    if (e == hipSuccess) e = hipMemcpy(&cnt, dcnt, sizeof cnt, hipMemcpyDeviceToHost);
-    (void)hipFree(buf);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double) * np, hipMemcpyDeviceToHost, c.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&cnt, dcnt, sizeof cnt, hipMemcpyDeviceToHost, c.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
     if (e != hipSuccess) return set_err(nullptr, TD_ERR_HIP, std::string("td_trilinear: ") + hipGetErrorString(e));
     *n_outside = (int64_t)cnt;
     return TD_OK;

@@ -74,6 +74,14 @@ class TdContext:
         check(lib().td_misfit(self.h, len(p), ptr(p), ptr(t), ptr(s), ctypes.byref(phi), ctypes.byref(lk)), self.h)
         return phi.value, lk.value
 
+    INCR_FULL, INCR_LAUNCH, INCR_RESIDENT = 0, 1, 2
+
+    def set_incremental(self, mode):
+        """td_evaluate's incremental path: INCR_RESIDENT (default: a resident
+        kernel answers every call), INCR_LAUNCH (one launch per call; use it when
+        other GPU work, e.g. a collective, runs between evaluates) or INCR_FULL."""
+        check(lib().td_set_incremental(self.h, int(mode)), self.h)
+
     NN_AUTO, NN_BRUTE, NN_GRID, NN_BRUTE_SPLIT = 0, 1, 2, 3
 
     def set_nn_method(self, method):

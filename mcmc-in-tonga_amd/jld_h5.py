@@ -350,7 +350,12 @@ def read_checkpoint(path):
     for fld in DS_FIELDS:
         v = rec[fld + "_"][()]
         if fld in DS_RANGES:
-            out["ds_" + fld + "_range"] = np.array([v["ref_"]["hi_"], v["step_"]["hi_"], v["len_"]], dtype=np.float64)
+            # Julia's StepRangeLen: r[i] = ref + (i - offset) * step in TwicePrecision (hi + lo);
+            # the first element is ref + (1 - offset) * step
+            ref = float(v["ref_"]["hi_"]) + float(v["ref_"]["lo_"])
+            step = float(v["step_"]["hi_"]) + float(v["step_"]["lo_"])
+            first = ref + (1 - int(v["offset_"])) * step
+            out["ds_" + fld + "_range"] = np.array([first, step, v["len_"]], dtype=np.float64)
         else:
             a = np.asarray(f[v][()], dtype=np.float64)
             out["ds_" + fld] = np.ascontiguousarray(a.T) if fld in DS_MATRICES else a

@@ -89,6 +89,10 @@ class RayShardedContext:
         # a rank with no rays keeps a one-ray context for td_misfit only
         make = make_context or TdContext.from_datastruct  # (tests inject a host stand-in for the CPU suite)
         self.local = make(sub_datastruct(ds, r0, r1) if r1 > r0 else sub_datastruct(ds, 0, 1), device)
+        # an allgather runs between this context's evaluates: no resident kernel may hold
+        # the collective's hardware queue (td_set_incremental), one launch per call instead
+        if hasattr(self.local, "set_incremental"):
+            self.local.set_incremental(TdContext.INCR_LAUNCH)
         self.P_local = self.local.P if r1 > r0 else 0
 
     def evaluate(self, cells):

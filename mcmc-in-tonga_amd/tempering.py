@@ -22,7 +22,9 @@ Replicas = ranks x chains per rank, so one GPU may hold several (global
 replica id g = rank * local + j).  The decision is a pure function of the
 gathered vector, the round and the seed (``decide_swaps``), so it is tested
 without any GPU (tests/test_tempering.py)."""
+import hashlib
 import math
+import time
 
 import numpy as np
 
@@ -46,12 +48,13 @@ def _mix64(x):
 
 def _uniform(seed, rnd, level):
     """u in (0, 1), a pure function of (seed, round, level): two SplitMix64
-    rounds over the key, then (k + 1/2) / 2^53 of the top 53 bits.  A few
+    rounds over the key, then (k + 1/2) / 2^52 of the top 52 bits (53 bits
+    could round (2^53 - 1) + 1/2 up to exactly 1).  A few
     integer operations (a numpy Philox Generator per draw cost ~25 us, a third
     of a tempering round at 8 replicas x 10 proposals)."""
     x = _mix64((int(seed) * 0x9E3779B97F4A7C15 + int(rnd)) & _M64)
     x = _mix64((x + int(level) * 0xD1B54A32D192ED03 + 1) & _M64)
-    return ((x >> 11) + 0.5) / 9007199254740992.0
+    return ((x >> 12) + 0.5) / 4503599627370496.0
 
 
 def swap_log_alpha(phi_a, phi_b, t_a, t_b):
@@ -112,7 +115,7 @@ class TemperingLadder:
     other ranks' replicas.  Chains need ``run(k)``, ``stats()['phi']`` and
     ``set_temperature(T)`` (``chain.Chain`` or any stand-in)."""
 
-    def __init__(self, chains, exchange=None, tmax=8.0, seed=12345):
+    def __init__(self, chains, exchange=None, tmax=8.0, seed=12345, resident=True):
         self.chains = list(chains)
         self.ex = exchange or Exchange()
         self.local = len(self.chains)
@@ -126,34 +129,64 @@ class TemperingLadder:
         self.accepted = np.zeros(max(self.R - 1, 0), dtype=np.int64)
         for j, ch in enumerate(self.chains):
             ch.set_temperature(float(self.temps[self.gid(j)]))
+        # the swap trace (gathered phis, new levels) of every round, hashed: equal ladders, equal digests
+        self._trace = hashlib.sha256()
+        self.gather_s = 0.0  # wall time spent in the allgather (the collective), all rounds
         # td_chain replicas of one context run in one launch, one workgroup each
         self.batch = self.local > 1 and all(hasattr(c, "h") and getattr(c, "ctx", None) is self.chains[0].ctx
                                             for c in self.chains)
+        # DEVICE td_chain replicas of one context: one launch resident across the rounds (td_rounds),
+        # the temperatures posted to it every round instead of a launch per round
+        self.resident = bool(resident) and self.local >= 1 and all(
+            hasattr(c, "h") and getattr(c, "ctx", None) is self.chains[0].ctx and
+            getattr(getattr(c, "params", None), "engine", None) == 0 for c in self.chains)
+        self.rounds = None
 
     def gid(self, j):
         return self.ex.rank * self.local + j
 
     def step(self, k):
         """k proposals on every local replica, then one swap round."""
-        if self.batch:
-            from .chain import run_batch
+        if self.resident:
+            if self.rounds is None:
+                from .chain import Rounds
 
-            run_batch(self.chains, k)  # all local replicas in one launch
+                self.rounds = Rounds(self.chains)
+            mine = self.rounds.run(k, [self.temps[self.levels[self.gid(j)]] for j in range(self.local)])
         else:
-            for ch in self.chains:
-                ch.run(k)
-        mine = np.array([ch.stats()["phi"] for ch in self.chains], dtype=np.float64)
+            if self.batch:
+                from .chain import run_batch
+
+                run_batch(self.chains, k)  # all local replicas in one launch
+            else:
+                for ch in self.chains:
+                    ch.run(k)
+            mine = np.array([ch.stats()["phi"] for ch in self.chains], dtype=np.float64)
+        t0 = time.perf_counter()
         allphi = self.ex.allgather(mine)
+        self.gather_s += time.perf_counter() - t0
         new, tried, acc = decide_swaps(allphi, self.levels, self.temps, self.rnd, self.seed)
+        self._trace.update(np.ascontiguousarray(allphi, dtype=np.float64).tobytes())
+        self._trace.update(np.ascontiguousarray(new, dtype=np.int64).tobytes())
         self.tried += tried
         self.accepted += acc
         for j, ch in enumerate(self.chains):
             g = self.gid(j)
-            if new[g] != self.levels[g]:
+            if new[g] != self.levels[g] and not self.resident:  # (resident: posted with the next round)
                 ch.set_temperature(float(self.temps[new[g]]))
         self.levels = new
         self.rnd += 1
         return allphi
+
+    def close(self):
+        """End the resident launch (the chains' counts and models are current after it)."""
+        if self.rounds is not None:
+            self.rounds.close()
+            self.rounds = None
+
+    def trace_digest(self):
+        """sha256 of every round's gathered phis and new levels so far."""
+        return self._trace.hexdigest()
 
     def cold_local(self):
         """Index of the local chain at T = 1, or None (another rank holds it)."""

@@ -1,0 +1,43 @@
+"""bench.py's N > 1 path, as the driver launches it (torch.distributed.run,
+one process per rank), rehearsed on one GPU: two ranks over gloo, both on
+device 0 (TD_BENCH_BACKEND=gloo TD_BENCH_DEVICE=0), reduced sizes.  The
+JSON line must carry the config-4 ranks block with a swap trace equal to the
+one-process ladder's, and the config-5 stress chains block (BASELINE configs
+4 and 5; main_inversion.jl:15, define_TDstructure.jl:56)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(420)
+def test_bench_two_ranks_gloo():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, TD_BENCH_BACKEND="gloo", TD_BENCH_DEVICE="0")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+           "--warmup", "0", "--iters-per-step", "500", "--no-cpu-baseline", "--no-full-evaluate", "--no-dropin",
+           "--batch-chains", "0", "--config4-rounds", "40", "--stress-iters", "100", "--no-phases"]
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=400, cwd=ROOT)
+    text = p.stdout.decode(errors="replace")
+    assert p.returncode == 0, text[-4000:]
+    line = [x for x in text.splitlines() if x.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["roofline"]["bound"] == "latency"
+    c4 = out["config4_ranks"]
+    assert c4["replicas"] == 2 and c4["trace_matches_single_process"] is True, c4
+    assert c4["proposals_per_s"] > 0 and c4["allgather_us_per_round"] > 0
+    sc = out["stress_chains"]
+    assert sc["chains"] == 2 and sc["proposals_per_s"] > 0
+    assert "stress_sharded" in out

@@ -270,3 +270,36 @@ def test_priors_device_follows_host(tt, ds, ctx, prior, ncells, iters, seed):
     m = dev.model()
     ptS, phi, _, _ = ctx.evaluate(m.cells())
     assert phi == m.phi and np.array_equal(ptS, m.ptS)
+
+
+def test_resident_rounds_equal_launch_per_round(tt, ds, ctx):
+    """td_rounds (one launch resident across the swap rounds, temperatures
+    posted through pinned memory) gives exactly the ladder of one
+    td_chain_run_batch launch per round -- also when the host pauses past the
+    launch's 200 ms idle watchdog between rounds (it returns and is started
+    again) and when a round size changes."""
+    import time
+
+    prm = tt.define_TDstructrure().replace(max_cells=600)
+    runs = []
+    for resident in (True, False):
+        chains = [make(tt, ctx, prm, tt.random_model(200 + 30 * j, 60 + j), 60 + j, tt.TD_ENGINE_DEVICE,
+                       chain=1 + j) for j in range(4)]
+        lad = tt.TemperingLadder(chains, tmax=8.0, seed=99, resident=resident)
+        assert lad.resident == resident
+        trace = []
+        for r in range(30):
+            k = 10 if r < 20 else 7
+            trace.append([list(lad.step(k)), list(lad.levels)])
+            if r in (5, 6, 17):
+                time.sleep(0.3)
+        lad.close()
+        runs.append((trace, [c.model() for c in chains], [c.stats() for c in chains], lad.trace_digest()))
+        for c in chains:
+            c.close()
+    (ta, ma, sa, da), (tb, mb, sb, db) = runs
+    assert ta == tb and da == db
+    for a, b, x, y in zip(ma, mb, sa, sb):
+        assert same_models(a, b)
+        assert x["phi"] == y["phi"] and x["accepted"] == y["accepted"] and x["proposed"] == y["proposed"]
+        assert x["iterations"] == y["iterations"] == 20 * 10 + 10 * 7

@@ -24,7 +24,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from tempering_worker import ladder_chains  # noqa: E402
 
-NREP, NCELLS, SWAP_EVERY, ROUNDS = 8, 2000, 10, 40
+NREP, NCELLS, SWAP_EVERY, ROUNDS = 8, 2000, 10, 320  # bench.py config4_tempering: 20 + 300 rounds
 
 
 def trace_of(tt, chains):

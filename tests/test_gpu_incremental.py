@@ -212,3 +212,94 @@ def test_sigma_change_drops_the_shadow(tt, ds):
             b.set_sigma(sig)
     a.close()
     b.close()
+
+
+def test_server_reissues_a_command_after_its_watchdog(tt, ds):
+    """The host is descheduled between its alive check and the post of a
+    command (tdt_set_server_post_delay > the kernel's 200 ms watchdog): the
+    kernel has returned, its pending proposal undone; the command is re-issued
+    to a new launch (with that proposal as a committed step when the host
+    accepted it) and the DROPIN chain still makes the HOST engine's moves."""
+    prm = tt.define_TDstructrure().replace(max_cells=500)
+    model = tt.random_model(300, 31)
+    ctxs = [tt.TdContext.from_datastruct(ds) for _ in range(2)]
+    chains = [tt.Chain(c, tt.chain_params(prm, None, seed=31, chain=1, engine=e), model)
+              for c, e in zip(ctxs, (tt.TD_ENGINE_DROPIN, tt.TD_ENGINE_HOST))]
+    chains[0].run(20)  # the server is up
+    assert tt.lib().tdt_set_server_post_delay(260) == 0
+    try:
+        chains[0].run(8)  # every command (evaluate and one-point query) meets an exited kernel
+    finally:
+        tt.lib().tdt_set_server_post_delay(0)
+    chains[0].run(40)
+    chains[1].run(68)
+    a, b = chains[0].stats(), chains[1].stats()
+    assert a["phi"] == b["phi"] and a["accepted"] == b["accepted"] and a["proposed"] == b["proposed"]
+    assert same_models(chains[0].model(), chains[1].model())
+    for ch in chains:
+        ch.close()
+    for c in ctxs:
+        c.close()
+
+
+def test_two_contexts_interleaved_keep_their_pace(tt, ds, ref_ctx):
+    """Two contexts of one process, each followed by its resident server,
+    called alternately (one Julia worker driving two chains): starting one
+    context's work stops the other's resident kernel first (servers_quiesce),
+    so no call waits behind a kernel on a shared hardware queue; every result
+    equals the full evaluate."""
+    import time
+
+    ctxs = [tt.TdContext.from_datastruct(ds) for _ in range(2)]
+    rng = np.random.default_rng(17)
+    box = tt.box()
+    cur = [tt.random_model(500, 17 + k).cells() for k in range(2)]
+    times = []
+    for step in range(150):
+        for k in range(2):
+            prop = edit(rng, cur[k], box)
+            t0 = time.perf_counter()
+            a = ctxs[k].evaluate(prop)
+            times.append(time.perf_counter() - t0)
+            b = ref_ctx.evaluate(prop)
+            assert a[1] == b[1] and np.array_equal(a[0], b[0])
+            if rng.random() < 0.5:
+                cur[k] = prop
+    times = np.array(times[10:])
+    assert np.median(times) < 5e-3 and np.mean(times) < 20e-3, (np.median(times), np.mean(times), times.max())
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.timeout(300)
+def test_collective_between_evaluates(tt, tmp_path):
+    """An RCCL all_gather between td_evaluate calls (a ray-sharded run's
+    pattern), in a fresh child process (world 1 on device 0): same phi in
+    modes 1 and 2; mode 1 (what RayShardedContext selects) keeps every call
+    short.  Mode 2's per-call times are printed: a resident kernel sharing the
+    collective's hardware queue would show as ~200 ms stalls."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    res = {}
+    for mode in (1, 2):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        out = tmp_path / ("m%d.json" % mode)
+        p = subprocess.run([sys.executable, "-u", os.path.join(here, "collective_worker.py"), str(port), str(out),
+                            str(mode)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
+        assert p.returncode == 0, p.stdout.decode(errors="replace")[-3000:]
+        res[mode] = json.load(open(out))
+    assert res[1]["phis"] == res[2]["phis"]
+    t1, t2 = np.array(res[1]["times"][5:]), np.array(res[2]["times"][5:])
+    print("per call (evaluate + all_gather): mode 1 median %.3f ms max %.3f ms; mode 2 median %.3f ms max %.3f ms"
+          % (1e3 * np.median(t1), 1e3 * t1.max(), 1e3 * np.median(t2), 1e3 * t2.max()))
+    assert np.median(t1) < 5e-3 and t1.max() < 0.1
