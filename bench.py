@@ -509,7 +509,7 @@ def full_evaluate(tt, ctx, model, N, reps=50):
     """The drop-in td_evaluate (MCsub.jl:123-185) on the same model, both
     nearest-cell methods: the bucket grid (default from 256 cells) and the
     reference-shaped brute force (every point x every cell), whose dominant
-    kernel nn_partial is FP64-VALU bound (no FMA: 39.3 TFLOP/s roof)."""
+    kernel nn_tile is FP64-VALU bound (no FMA: 39.3 TFLOP/s roof)."""
     cells = model.cells()
     E = ctx.P * N
     out = {}
@@ -537,8 +537,7 @@ def full_evaluate(tt, ctx, model, N, reps=50):
                      "nn_pair_evals_per_s_equiv": round(E / el, 1), "kernel_ms": km}
     ctx.set_nn_method(ctx.NN_AUTO)
     tt.lib().tdt_set_incremental(ctx.h, 1)
-    # the dominant kernel: the one-launch tile search where the points fit a lane each per CU, else the
-    # split search (whose merge launch is reported beside it)
+    # the dominant kernel: the one-launch tile search (the split search only when forced)
     km = out["brute_force"]["kernel_ms"]
     kname = "nn_tile" if "nn_tile" in km else "nn_partial"
     t_nn = km.get(kname, 0.0) / 1e3
@@ -547,7 +546,7 @@ def full_evaluate(tt, ctx, model, N, reps=50):
     out["brute_force"]["roofline"] = {"kernel": kname, "bound": "valu-fp64", "achieved": round(tf, 3),
                                       "peak": FP64_NOFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                       "frac": round(tf / FP64_NOFMA_PEAK_TFLOPS, 4), "flops_per_launch": flops}
-    tr, src, _ = measured_traffic("k_%s/config3" % kname) if ctx.P < 100000 else (None, None, None)
+    tr, src, _ = measured_traffic("k_%s/%s" % (kname, "config3" if ctx.P < 100000 else "stress"))
     if tr is not None:
         out["brute_force"]["roofline"]["traffic"] = tr
         out["brute_force"]["roofline"]["traffic_source"] = src
@@ -639,8 +638,20 @@ def posterior_maps(tt, ctx, ds):
     el = (time.perf_counter() - t0) / reps
     nl, kms = ctx.timing(kernel="raster_brute")
     ctx.timing(enable=False)
+    flops = 8.0 * len(qx) * ncells * len(models)  # 3 sub + 3 mul + 2 add per distance, no FMA
+    k_s = kms / 1e3 / max(nl, 1) if nl else 0.0
+    tf = flops / k_s / 1e12 if k_s > 0 else 0.0
+    roof = {"kernel": "k_raster_brute", "bound": "valu-fp64", "achieved": round(tf, 3),
+            "peak": FP64_NOFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / FP64_NOFMA_PEAK_TFLOPS, 4),
+            "flops_per_launch": flops,
+            # every model's cells x, y, z once, its zeta per node, the nodes, the values written
+            "compulsory_bytes": 24 * ncells * len(models) + 8 * len(qx) * len(models) + 24 * len(qx) +
+                                8 * len(qx) * len(models)}
+    tr, src, _ = measured_traffic("k_raster_brute/section")
+    if tr is not None and len(models) == 100 and ncells == 5000:
+        roof["traffic"], roof["traffic_source"] = tr, src
     return {"nodes": int(len(qx)), "models": len(models), "cells": ncells, "ms_per_section": round(el * 1e3, 3),
-            "kernel_ms_per_section": round(kms / max(nl, 1), 4) if nl else None,
+            "kernel_ms_per_section": round(kms / max(nl, 1), 4) if nl else None, "roofline": roof,
             "note": "ms_per_section: the whole call from host arrays (cells packed into pinned memory, one copy); "
                     "kernel: every model at every node in one launch (k_raster_brute)",
             "node_model_pairs_per_s": round(len(qx) * len(models) / el, 1),

@@ -23,6 +23,41 @@ namespace tdstar {
 
 constexpr double kSentinel = 1e9;  // MCsub.jl:250
 
+// One group step of the brute-force scans (k_nn_tile, k_nn_partial,
+// k_raster_brute): the distances dg[k][u] of PPL points to 8 consecutive cells
+// base .. base + 7 update each point's running (bd, bi) under v_nearest's
+// strict '<' in index order (MCsub.jl:255).  The group minimum is a tree of
+// v_min (fmin: a NaN distance never becomes the minimum; the same value as the
+// left-to-right chain, with 3 dependent steps instead of 7); every point's
+// minimum is formed before ONE branch, taken only when some point improves
+// (rare after the first groups), where the first cell reaching the minimum is
+// looked up.  A group tie goes to its first cell, a tie with an earlier group
+// keeps the earlier cell -- exactly the sequential strict '<' scan.
+template <int PPL>
+__device__ __forceinline__ void group8_update(const double (&dg)[PPL][8], double (&bd)[PPL], int (&bi)[PPL],
+                                              int base) {
+    double m[PPL];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        const double a = fmin(fmin(dg[k][0], dg[k][1]), fmin(dg[k][2], dg[k][3]));
+        const double b = fmin(fmin(dg[k][4], dg[k][5]), fmin(dg[k][6], dg[k][7]));
+        m[k] = fmin(a, b);
+        any = any || m[k] < bd[k];  // strict: NaN never wins
+    }
+    if (any) {
+#pragma unroll
+        for (int k = 0; k < PPL; ++k)
+            if (m[k] < bd[k]) {
+                int f = 7;
+#pragma unroll
+                for (int u = 7; u >= 0; --u) f = dg[k][u] == m[k] ? u : f;
+                bd[k] = m[k];
+                bi[k] = base + f;
+            }
+    }
+}
+
 // Per-kernel timing with HIP events recorded on the launch stream (bench.py's
 // roofline numbers).  Disabled: begin()/end() are no-ops.
 struct Timer {
@@ -99,7 +134,7 @@ constexpr int kGridCap = 16;               // entries per bucket (a fuller bucke
 constexpr int kGridMinCells = 256;     // below: the brute force is as fast
 
 // Workspace for the nearest searches (split brute force; bucket grid).
-constexpr int kNNAuto = 0;   // brute force: k_nn_tile when the points fit one lane each per CU
+constexpr int kNNAuto = 0;   // brute force: k_nn_tile (every point count up to ~128 M)
 constexpr int kNNSplit = 1;  // brute force: always the split search (k_nn_partial + k_nn_merge)
 
 struct NNWork {
@@ -132,11 +167,12 @@ struct NNPlan {
 };
 NNPlan plan_nearest(int64_t npts, int64_t ncells, int num_cus);
 
-// The one-launch brute force (k_nn_tile): one workgroup per CU owns Q points
-// and scans every cell for them in S slices of L cells, staged R at a time.
+// The one-launch brute force (k_nn_tile): tiles of Q points, one workgroup
+// per CU taking every gridDim-th tile; a tile's points are checked against
+// every cell in S slices of L cells, staged R at a time.
 struct TilePlan {
-    bool ok = false;  // false: too many points per CU, use the split search
-    int Q = 0, S = 0, L = 0, R = 0, blocks = 0, ppl = 2;
+    bool ok = false;  // false: no tile shape fits (the split search)
+    int Q = 0, S = 0, L = 0, R = 0, tiles = 0, blocks = 0, ppl = 2;
     size_t lds = 0;
 };
 TilePlan plan_tile(int64_t npts, int64_t ncells, int num_cus);

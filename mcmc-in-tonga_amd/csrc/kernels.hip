@@ -67,15 +67,11 @@ __global__ __launch_bounds__(kNNThreads) void k_nn_partial(
 
     // groups of kGroup cells: the group minimum takes one v_min per distance
     // (instead of compare + three selects); only when it beats the running
-    // best is the first cell reaching it looked up -- rare after the first
-    // groups.  Exactly MCsub.jl:255's strict '<' in index order: the minimum
-    // is one of the distances, a tie inside the group goes to its first cell,
-    // a tie with an earlier group keeps the earlier cell.
+    // best is the first cell reaching it looked up (group8_update, internal.h)
     constexpr int kGroup = 8;
     int j = 0;
     for (; j + kGroup <= nc; j += kGroup) {
         double dg[PPL][kGroup];
-        double m[PPL];
 #pragma unroll
         for (int u = 0; u < kGroup; ++u) {
             const double4 c = sc[j + u];
@@ -87,18 +83,9 @@ __global__ __launch_bounds__(kNNThreads) void k_nn_partial(
                 d = d + dy * dy;
                 d = d + dz * dz;
                 dg[k][u] = d;
-                m[k] = u == 0 ? d : fmin(m[k], d);  // fmin: a NaN distance never becomes the minimum
             }
         }
-#pragma unroll
-        for (int k = 0; k < PPL; ++k)
-            if (m[k] < bd[k]) {  // strict: NaN never wins
-                int f = kGroup - 1;
-#pragma unroll
-                for (int u = kGroup - 1; u >= 0; --u) f = dg[k][u] == m[k] ? u : f;
-                bd[k] = m[k];
-                bi[k] = c0 + j + f;
-            }
+        group8_update<PPL>(dg, bd, bi, c0 + j);
     }
     for (; j < nc; ++j) {  // the tail, one cell at a time
         const double4 c = sc[j];
@@ -124,17 +111,22 @@ __global__ __launch_bounds__(kNNThreads) void k_nn_partial(
 }
 
 // ---------------------------------------------------------------------------
-// Stage 1 (one launch, no partials): k_nn_tile.  One 1024-thread workgroup
-// per CU owns Q = ceil(P / CUs) points and scans EVERY cell for them, so the
-// chip is balanced to within one point per CU and nothing but the answer
-// leaves the CU.  Lane t takes point t % Q and cell slice t / Q (S slices of
-// L cells, S * Q <= 1024): the slices are merged in LDS in slice order at the
-// end, so the lowest cell index wins a tie exactly as in the sequential scan.
-// Cells are staged in rounds of R per slice, SoA with an odd stride (R + 1
-// doubles: two slices read by one lane group never share a bank), double
-// buffered with one barrier per round; the next round's global loads are in
-// flight while the current round is scanned.  The tail of a round is padded
-// with NaN cells: fmin and the strict '<' never pick them.
+// Stage 1 (one launch, no partials): k_nn_tile.  The points are cut into
+// equal tiles of Q points; one 1024-thread workgroup per CU (grid = min(tiles,
+// CUs)) takes tiles blockIdx.x, blockIdx.x + gridDim.x, ... and scans EVERY
+// cell for each, so nothing but the answer leaves the CU and the chip is
+// balanced to within one tile (the planner picks Q so every CU holds about the
+// same number of tiles: one tile per CU up to 2048 points per CU, several for
+// the stress geometry's 584k points).  Lane t takes point group t % Qg and
+// cell slice t / Qg (S slices of L cells, S * Qg <= 1024): the slices are
+// merged in LDS in slice order at the end of a tile, so the lowest cell index
+// wins a tie exactly as in the sequential scan.  Cells are staged in rounds of
+// R per slice, SoA with an odd stride (R + 1 doubles: two slices read by one
+// lane group never share a bank), double buffered with one barrier per round;
+// the next round's global loads are in flight while the current round is
+// scanned.  The tail of a round is padded with NaN cells: fmin and the strict
+// '<' never pick them.  Traffic: the points once, the cells once per XCD (L2),
+// the answers once -- no per-chunk partials, no merge launch.
 // ---------------------------------------------------------------------------
 constexpr int kTileThreads = 1024;
 
@@ -142,16 +134,16 @@ template <int PPL>
 __global__ __launch_bounds__(kTileThreads) void k_nn_tile(
     const double *__restrict__ qx, const double *__restrict__ qy, const double *__restrict__ qz,
     int npts, int ys, int zs, const double *__restrict__ cells, int stride, int ncells, int Q, int S, int L,
-    int R, int *__restrict__ best_i, double *__restrict__ best_d, double *__restrict__ zeta0) {
-    extern __shared__ double lds[];  // [2 buffers][3 fields: x, y, z][S][R + 1]
+    int R, int ntiles, int *__restrict__ best_i, double *__restrict__ best_d, double *__restrict__ zeta0) {
+    extern __shared__ double lds[];  // [2 buffers][3 fields: x, y, z][S][R + 1]; the merge reuses it
     const int RS = R + 1;
     const int buf_sz = 3 * S * RS;
     const int t = threadIdx.x;
     const int Qg = (Q + PPL - 1) / PPL;  // point groups: lane g takes points g, g + Qg, ... of the tile
     const int g = t % Qg, s = t / Qg;
-    const int p0 = blockIdx.x * Q;
     const int rounds = (L + R - 1) / R;
     const int nstage = S * R;  // cells staged per round
+    const bool active = s < S;
 
     // one cell of round r for staging element e (slice e / R, offset e % R), NaN past the slice / cell set
     auto fetch = [&](int r, int e, double &cx, double &cy, double &cz) {
@@ -173,116 +165,109 @@ __global__ __launch_bounds__(kTileThreads) void k_nn_tile(
         buf[(2 * S + ss) * RS + j] = cz;
     };
     constexpr int kStageMax = 2;  // staging elements per thread (S * R <= 2048)
-    double sx[kStageMax], sy[kStageMax], sz[kStageMax];
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int p0 = tile * Q;
+        double sx[kStageMax], sy[kStageMax], sz[kStageMax];
 #pragma unroll
-    for (int k = 0; k < kStageMax; ++k) {  // round 0's cells and the points: one round trip
-        const int e = t + k * kTileThreads;
-        if (e < nstage) fetch(0, e, sx[k], sy[k], sz[k]);
-    }
-    double x[PPL], y[PPL], z[PPL], bd[PPL];
-    int bi[PPL];
-#pragma unroll
-    for (int k = 0; k < PPL; ++k) {
-        const int p = min(p0 + min(g + k * Qg, Q - 1), npts - 1);
-        x[k] = qx[p];
-        y[k] = qy[(long)p * ys];
-        z[k] = qz[(long)p * zs];
-        bd[k] = kSentinel;
-        bi[k] = -1;
-    }
-#pragma unroll
-    for (int k = 0; k < kStageMax; ++k) {
-        const int e = t + k * kTileThreads;
-        if (e < nstage) put(lds, e, sx[k], sy[k], sz[k]);
-    }
-    __syncthreads();
-    const bool active = s < S;
-    for (int r = 0; r < rounds; ++r) {
-        const bool more = r + 1 < rounds;
-        if (more) {
-#pragma unroll
-            for (int k = 0; k < kStageMax; ++k) {
-                const int e = t + k * kTileThreads;
-                if (e < nstage) fetch(r + 1, e, sx[k], sy[k], sz[k]);
-            }
+        for (int k = 0; k < kStageMax; ++k) {  // round 0's cells and the points: one round trip
+            const int e = t + k * kTileThreads;
+            if (e < nstage) fetch(0, e, sx[k], sy[k], sz[k]);
         }
-        if (active) {
-            const double *bx = lds + (r & 1) * buf_sz + s * RS;
-            const double *by = bx + S * RS;
-            const double *bz = by + S * RS;
-            const int cbase = s * L + r * R;
-            // groups of 8: one v_min per distance; the first cell reaching a new best is looked up only
-            // when the group beats it (MCsub.jl:255 strict '<' in index order)
-            for (int j = 0; j < R; j += 8) {
-                double dg[PPL][8];
-                double m[PPL];
+        double x[PPL], y[PPL], z[PPL], bd[PPL];
+        int bi[PPL];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const double cx = bx[j + u], cy = by[j + u], cz = bz[j + u];
+        for (int k = 0; k < PPL; ++k) {
+            const int p = min(p0 + min(g + k * Qg, Q - 1), npts - 1);
+            x[k] = qx[p];
+            y[k] = qy[(long)p * ys];
+            z[k] = qz[(long)p * zs];
+            bd[k] = kSentinel;
+            bi[k] = -1;
+        }
+        __syncthreads();  // the previous tile's merge has read the LDS
 #pragma unroll
-                    for (int k = 0; k < PPL; ++k) {
-                        // (mx[i]-x)^2 + (my[i]-y)^2 + (mz[i]-z)^2, MCsub.jl:254, left to right, unfused
-                        const double dx = cx - x[k], dy = cy - y[k], dz = cz - z[k];
-                        double d = dx * dx;
-                        d = d + dy * dy;
-                        d = d + dz * dz;
-                        dg[k][u] = d;
-                        m[k] = u == 0 ? d : fmin(m[k], d);
-                    }
+        for (int k = 0; k < kStageMax; ++k) {
+            const int e = t + k * kTileThreads;
+            if (e < nstage) put(lds, e, sx[k], sy[k], sz[k]);
+        }
+        __syncthreads();
+        for (int r = 0; r < rounds; ++r) {
+            const bool more = r + 1 < rounds;
+            if (more) {
+#pragma unroll
+                for (int k = 0; k < kStageMax; ++k) {
+                    const int e = t + k * kTileThreads;
+                    if (e < nstage) fetch(r + 1, e, sx[k], sy[k], sz[k]);
                 }
-#pragma unroll
-                for (int k = 0; k < PPL; ++k)
-                    if (m[k] < bd[k]) {
-                        int f = 7;
-#pragma unroll
-                        for (int u = 7; u >= 0; --u) f = dg[k][u] == m[k] ? u : f;
-                        bd[k] = m[k];
-                        bi[k] = cbase + j + f;
-                    }
             }
-        }
-        if (more) {
-            double *nb = lds + ((r + 1) & 1) * buf_sz;
+            if (active) {
+                const double *bx = lds + (r & 1) * buf_sz + s * RS;
+                const double *by = bx + S * RS;
+                const double *bz = by + S * RS;
+                const int cbase = s * L + r * R;
+                // groups of 8: one v_min per distance; the first cell reaching a new best is looked up only
+                // when the group beats it (MCsub.jl:255 strict '<' in index order; group8_update)
+                for (int j = 0; j < R; j += 8) {
+                    double dg[PPL][8];
 #pragma unroll
-            for (int k = 0; k < kStageMax; ++k) {
-                const int e = t + k * kTileThreads;
-                if (e < nstage) put(nb, e, sx[k], sy[k], sz[k]);
+                    for (int u = 0; u < 8; ++u) {
+                        const double cx = bx[j + u], cy = by[j + u], cz = bz[j + u];
+#pragma unroll
+                        for (int k = 0; k < PPL; ++k) {
+                            // (mx[i]-x)^2 + (my[i]-y)^2 + (mz[i]-z)^2, MCsub.jl:254, left to right, unfused
+                            const double dx = cx - x[k], dy = cy - y[k], dz = cz - z[k];
+                            double d = dx * dx;
+                            d = d + dy * dy;
+                            d = d + dz * dz;
+                            dg[k][u] = d;
+                        }
+                    }
+                    group8_update<PPL>(dg, bd, bi, cbase + j);
+                }
+            }
+            if (more) {
+                double *nb = lds + ((r + 1) & 1) * buf_sz;
+#pragma unroll
+                for (int k = 0; k < kStageMax; ++k) {
+                    const int e = t + k * kTileThreads;
+                    if (e < nstage) put(nb, e, sx[k], sy[k], sz[k]);
+                }
+            }
+            __syncthreads();
+        }
+        // merge the slices in slice order (strict '<': the lower slice, hence the lower index, keeps a tie)
+        double *md = lds;                                // [S][Q]
+        int *mi = reinterpret_cast<int *>(lds + S * Q);  // [S][Q]
+        if (active) {
+#pragma unroll
+            for (int k = 0; k < PPL; ++k) {
+                const int qq = g + k * Qg;
+                if (qq < Q) {
+                    md[s * Q + qq] = bd[k];
+                    mi[s * Q + qq] = bi[k];
+                }
             }
         }
         __syncthreads();
-    }
-    // merge the slices in slice order (strict '<': the lower slice, hence the lower index, keeps a tie)
-    double *md = lds;                                // [S][Q]
-    int *mi = reinterpret_cast<int *>(lds + S * Q);  // [S][Q]
-    if (active) {
+        for (int qq = t; qq < Q && p0 + qq < npts; qq += kTileThreads) {
+            double d = md[qq];
+            int ks = 0;
+            for (int k0 = 1; k0 < S; k0 += 8) {  // eight slices' distances in flight, then compared in order
+                double dk[8];
 #pragma unroll
-        for (int k = 0; k < PPL; ++k) {
-            const int qq = g + k * Qg;
-            if (qq < Q) {
-                md[s * Q + qq] = bd[k];
-                mi[s * Q + qq] = bi[k];
+                for (int u = 0; u < 8; ++u) dk[u] = k0 + u < S ? md[(k0 + u) * Q + qq] : kSentinel;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (dk[u] < d) {
+                        d = dk[u];
+                        ks = k0 + u;
+                    }
             }
+            const int pp = p0 + qq, i = mi[ks * Q + qq];
+            if (best_i) best_i[pp] = i;
+            if (best_d) best_d[pp] = d;
+            if (zeta0) zeta0[pp] = i >= 0 ? cells[3 * stride + i] : 0.0;  // MCsub.jl:249 v = 0 when nothing < 1e9
         }
-    }
-    __syncthreads();
-    for (int qq = t; qq < Q && p0 + qq < npts; qq += kTileThreads) {
-        double d = md[qq];
-        int ks = 0;
-        for (int k0 = 1; k0 < S; k0 += 8) {  // eight slices' distances in flight, then compared in order
-            double dk[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) dk[u] = k0 + u < S ? md[(k0 + u) * Q + qq] : kSentinel;
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (dk[u] < d) {
-                    d = dk[u];
-                    ks = k0 + u;
-                }
-        }
-        const int pp = p0 + qq, i = mi[ks * Q + qq];
-        if (best_i) best_i[pp] = i;
-        if (best_d) best_d[pp] = d;
-        if (zeta0) zeta0[pp] = i >= 0 ? cells[3 * stride + i] : 0.0;  // MCsub.jl:249 v = 0 when nothing < 1e9
     }
 }
 
@@ -567,39 +552,56 @@ NNPlan plan_nearest(int64_t npts, int64_t ncells, int num_cus) {
 }
 
 TilePlan plan_tile(int64_t npts, int64_t ncells, int num_cus) {
-    TilePlan t{};
+    TilePlan best{};
     const int64_t G = std::max(num_cus, 1);
-    if (npts <= 0 || ncells <= 0) return t;
-    const int64_t Q = (npts + G - 1) / G;
+    if (npts <= 0 || ncells <= 0) return best;
     constexpr int ppl = 2;  // points per lane (measured against 1: tools/nn_bench2.py)
     constexpr int fields = 3;
-    const int64_t Qg = (Q + ppl - 1) / ppl;
-    if (Qg > kTileThreads) return t;  // more points than lanes per CU: the split search
-    int64_t S = std::min<int64_t>(kTileThreads / Qg, 256);  // <= 256 slices: S * 8 <= 2048 staged cells
-    S = std::min<int64_t>(S, (ncells + 7) / 8);              // >= 8 cells per slice
-    S = std::max<int64_t>(S, 1);
-    const int64_t L = (ncells + S - 1) / S;
-    S = (ncells + L - 1) / L;                                // no empty slice
-    // lanes busy: below ~70 % the split search does better on large point sets
-    if (Q * S * 10 < (int64_t)kTileThreads * ppl * 7 && npts >= 65536) return t;
-    // rounds: as many cells as the staging registers (2 per thread) and the LDS (double buffered) hold
-    int64_t rmax = std::min<int64_t>(64, (2048 / S) / 8 * 8);
-    rmax = std::min<int64_t>(rmax, ((int64_t)(150 * 1024) / (2 * fields * 8 * S) - 1) / 8 * 8);
-    rmax = std::max<int64_t>(rmax, 8);
-    const int64_t rounds = (L + rmax - 1) / rmax;
-    const int64_t R = ((L + rounds - 1) / rounds + 7) / 8 * 8;
-    t.ok = true;
-    t.Q = (int)Q;
-    t.S = (int)S;
-    t.L = (int)L;
-    t.R = (int)R;
-    t.ppl = ppl;
-    t.blocks = (int)((npts + Q - 1) / Q);
-    t.lds = std::max<size_t>((size_t)2 * fields * S * (R + 1) * sizeof(double),
-                             (size_t)S * Q * (sizeof(double) + sizeof(int)));
-    // more than half the CU's LDS: one workgroup per CU, never two on one CU while another idles
-    t.lds = std::max<size_t>(t.lds, 81 * 1024);
-    return t;
+    // tiles per CU m = 1, 2, ...: a tile of Q points is S * Qg lanes (Qg = Q / ppl point groups, S
+    // cell slices of L cells); estimated cycles per CU = its tiles x (the busiest SIMD's waves x the
+    // distances a lane computes x ~40 cycles each + a tile's fixed cost: first round trip, slice merge)
+    double best_cost = 0.0;
+    for (int64_t m = 1; m <= 256; ++m) {
+        const int64_t Q = (npts + G * m - 1) / (G * m);
+        const int64_t Qg = (Q + ppl - 1) / ppl;
+        if (Qg > kTileThreads) continue;
+        int64_t S = std::min<int64_t>(kTileThreads / Qg, 256);  // <= 256 slices: S * 8 <= 2048 staged cells
+        S = std::min<int64_t>(S, (ncells + 7) / 8);              // >= 8 cells per slice
+        S = std::max<int64_t>(S, 1);
+        const int64_t L = (ncells + S - 1) / S;
+        S = (ncells + L - 1) / L;  // no empty slice
+        const int64_t tiles = (npts + Q - 1) / Q;
+        const int64_t per_cu = (tiles + G - 1) / G;
+        const int64_t waves = (Qg * S + 63) / 64;
+        const double cost = (double)per_cu * ((double)((waves + 3) / 4) * ppl * (double)L * 40.0 + 12000.0);
+        if (best.ok && cost >= best_cost) {
+            if (Q < 64) break;  // tiles only get smaller and dearer from here
+            continue;
+        }
+        // rounds: as many cells as the staging registers (2 per thread) and the LDS (double buffered) hold
+        int64_t rmax = std::min<int64_t>(64, (2048 / S) / 8 * 8);
+        rmax = std::min<int64_t>(rmax, ((int64_t)(150 * 1024) / (2 * fields * 8 * S) - 1) / 8 * 8);
+        rmax = std::max<int64_t>(rmax, 8);
+        const int64_t rounds = (L + rmax - 1) / rmax;
+        const int64_t R = ((L + rounds - 1) / rounds + 7) / 8 * 8;
+        const size_t lds = std::max<size_t>((size_t)2 * fields * S * (R + 1) * sizeof(double),
+                                            (size_t)S * Q * (sizeof(double) + sizeof(int)));
+        if (lds > 160 * 1024) continue;
+        TilePlan t{};
+        t.ok = true;
+        t.Q = (int)Q;
+        t.S = (int)S;
+        t.L = (int)L;
+        t.R = (int)R;
+        t.ppl = ppl;
+        t.tiles = (int)tiles;
+        t.blocks = (int)std::min<int64_t>(tiles, G);
+        // more than half the CU's LDS: one workgroup per CU, never two on one CU while another idles
+        t.lds = std::max<size_t>(lds, 81 * 1024);
+        best = t;
+        best_cost = cost;
+    }
+    return best;
 }
 
 hipError_t launch_nearest(const double *qx, const double *qy, const double *qz, int64_t npts,
@@ -621,7 +623,7 @@ hipError_t launch_nearest(const double *qx, const double *qy, const double *qz, 
             }
             hipLaunchKernelGGL(kern, dim3((unsigned)tp.blocks), dim3(kTileThreads), tp.lds, s, qx, qy, qz,
                                (int)npts, (int)qy_stride, (int)qz_stride, cells, (int)stride, (int)ncells, tp.Q, tp.S,
-                               tp.L, tp.R, best_i, best_d, zeta0);
+                               tp.L, tp.R, tp.tiles, best_i, best_d, zeta0);
             if (tm) tm->end("nn_tile", t0, s);
             return hipGetLastError();
         }

@@ -67,71 +67,127 @@ __device__ double julia_mapreduce_seq_blocks(F f, int n) {
 }
 
 // Every model at every node in ONE launch (the section's nodes are few; one
-// launch group per model cost ~80 us of launches and host work per model):
-// grid (node chunks, models).  A workgroup stages its model's cells through LDS
-// in chunks (x, y, z SoA), each lane keeps its node's running (distance, index)
-// with v_nearest's strict '<' in index order (MCsub.jl:250-258: the first
-// minimum wins, only distances below the 1e9 sentinel count; NaN never wins);
-// groups of 8 cells take one v_min per distance and look the index up only
-// when the group beats the running best.  The value is zeta of the winner, or
-// 0.0 when none (MCsub.jl:249).
-constexpr int kRasterThreads = 256;
-constexpr int kRasterChunk = 2048;  // cells per LDS chunk: 48 KB
+// launch group per model cost ~80 us of launches and host work per model).
+// A work item = (model, chunk of kRasterNodes nodes); a 512-thread workgroup
+// is 8 waves = 8 slices of the model's cells, each lane 2 nodes of the chunk
+// (100 models x 16 chunks x 8 waves: 13 waves per SIMD, no partial last wave).
+// The cells a wave reads are the same in every lane, so they come through the
+// scalar cache (wave-uniform addresses: s_load, SGPR operands) -- no LDS
+// staging, no barrier but the final one.  Each lane keeps its nodes' running
+// (distance, index) with v_nearest's strict '<' in index order (MCsub.jl:
+// 250-258: the first minimum wins, only distances below the 1e9 sentinel
+// count; NaN never wins); groups of 8 cells take one v_min per distance and
+// look the index up only when the group beats the running best.  The slices
+// are merged in slice order (a tie keeps the lower slice, hence the lower
+// index).  The value is zeta of the winner, or 0.0 when none (MCsub.jl:249).
+// XCD-aware mapping: the dispatcher deals workgroups round-robin over the 8
+// XCDs, so block L runs on XCD L % 8; every chunk of model m is given to a
+// block of XCD m % 8, and each model's cells are fetched from HBM into ONE L2.
+constexpr int kRasterThreads = 512;
+constexpr int kRasterSlices = kRasterThreads / 64;
+constexpr int kRasterPPL = 2;
+constexpr int kRasterNodes = 64 * kRasterPPL;
+constexpr int kXcds = 8;
 __global__ __launch_bounds__(kRasterThreads) void k_raster_brute(const int64_t *__restrict__ cell_off,
                                                                  const double *__restrict__ cells, int64_t cs,
-                                                                 const double *__restrict__ q, int nq,
-                                                                 double *__restrict__ values) {
-    __shared__ double sx[kRasterChunk], sy[kRasterChunk], sz[kRasterChunk];
-    const int m = blockIdx.y;
+                                                                 const double *__restrict__ q, int nq, int nmodels,
+                                                                 int nchunks, double *__restrict__ values) {
+    __shared__ double md[kRasterSlices][kRasterNodes];
+    __shared__ int mi[kRasterSlices][kRasterNodes];
+    const int L = blockIdx.x, xcd = L % kXcds, j = L / kXcds;
+    const int m = xcd + kXcds * (j / nchunks), chunk = j % nchunks;
+    if (m >= nmodels) return;  // the whole workgroup: no barrier reached
     const long a = (long)cell_off[m];
     const int nc = (int)(cell_off[m + 1] - a);
-    const int node = blockIdx.x * kRasterThreads + threadIdx.x;
-    const int nd = min(node, nq - 1);
-    const double x = q[nd], y = q[nq + nd], z = q[2 * (long)nq + nd];
-    double bd = kSentinel;
-    int bi = -1;
-    for (int c0 = 0; c0 < nc; c0 += kRasterChunk) {
-        const int n = min(kRasterChunk, nc - c0);
-        __syncthreads();  // the previous chunk is read
-        for (int j = threadIdx.x; j < n; j += kRasterThreads) {
-            sx[j] = cells[a + c0 + j];
-            sy[j] = cells[cs + a + c0 + j];
-            sz[j] = cells[2 * cs + a + c0 + j];
-        }
-        __syncthreads();
-        int j = 0;
-        for (; j + 8 <= n; j += 8) {
-            double dg[8], mg;
+    const int lane = threadIdx.x & 63;
+    const int sl = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int per = (nc + kRasterSlices - 1) / kRasterSlices;
+    const int c_lo = min(sl * per, nc), c_hi = min(c_lo + per, nc);
+    const double *__restrict__ cx = cells + a, *__restrict__ cy = cells + cs + a, *__restrict__ cz = cells + 2 * cs + a;
+    double x[kRasterPPL], y[kRasterPPL], z[kRasterPPL], bd[kRasterPPL];
+    int bi[kRasterPPL];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+    for (int k = 0; k < kRasterPPL; ++k) {
+        const int nd = min(chunk * kRasterNodes + k * 64 + lane, nq - 1);
+        x[k] = q[nd];
+        y[k] = q[nq + nd];
+        z[k] = q[2 * (long)nq + nd];
+        bd[k] = kSentinel;
+        bi[k] = -1;
+    }
+    int c = c_lo;
+    // the next group's cells are loaded (scalar loads, wave-uniform) while this group is scanned
+    double ux[8], uy[8], uz[8];
+    if (c + 8 <= c_hi) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            ux[u] = cx[c + u];
+            uy[u] = cy[c + u];
+            uz[u] = cz[c + u];
+        }
+    }
+    for (; c + 8 <= c_hi; c += 8) {
+        double vx[8], vy[8], vz[8];
+        const int cn = c + 8 + 8 <= c_hi ? c + 8 : c;  // (the last group reloads itself: no branch)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            vx[u] = cx[cn + u];
+            vy[u] = cy[cn + u];
+            vz[u] = cz[cn + u];
+        }
+        double dg[kRasterPPL][8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+#pragma unroll
+            for (int k = 0; k < kRasterPPL; ++k) {
                 // (mx[i]-x)^2 + (my[i]-y)^2 + (mz[i]-z)^2, MCsub.jl:254, left to right, unfused
-                const double dx = sx[j + u] - x, dy = sy[j + u] - y, dz = sz[j + u] - z;
+                const double dx = ux[u] - x[k], dy = uy[u] - y[k], dz = uz[u] - z[k];
                 double d = dx * dx;
                 d = d + dy * dy;
                 d = d + dz * dz;
-                dg[u] = d;
-                mg = u == 0 ? d : fmin(mg, d);  // fmin: a NaN distance never becomes the minimum
-            }
-            if (mg < bd) {  // strict: NaN never wins
-                int f = 7;
-#pragma unroll
-                for (int u = 7; u >= 0; --u) f = dg[u] == mg ? u : f;
-                bd = mg;
-                bi = c0 + j + f;
+                dg[k][u] = d;
             }
         }
-        for (; j < n; ++j) {
-            const double dx = sx[j] - x, dy = sy[j] - y, dz = sz[j] - z;
+        group8_update<kRasterPPL>(dg, bd, bi, c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            ux[u] = vx[u];
+            uy[u] = vy[u];
+            uz[u] = vz[u];
+        }
+    }
+    for (; c < c_hi; ++c) {
+        const double ux = cx[c], uy = cy[c], uz = cz[c];
+#pragma unroll
+        for (int k = 0; k < kRasterPPL; ++k) {
+            const double dx = ux - x[k], dy = uy - y[k], dz = uz - z[k];
             double d = dx * dx;
             d = d + dy * dy;
             d = d + dz * dz;
-            if (d < bd) {
-                bd = d;
-                bi = c0 + j;
+            if (d < bd[k]) {
+                bd[k] = d;
+                bi[k] = c;
             }
         }
     }
-    if (node < nq) values[(long)m * nq + node] = bi >= 0 ? cells[3 * cs + a + bi] : 0.0;
+#pragma unroll
+    for (int k = 0; k < kRasterPPL; ++k) {
+        md[sl][k * 64 + lane] = bd[k];
+        mi[sl][k * 64 + lane] = bi[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < kRasterNodes) {
+        const int t = threadIdx.x, node = chunk * kRasterNodes + t;
+        double d = md[0][t];
+        int i = mi[0][t];
+#pragma unroll
+        for (int s2 = 1; s2 < kRasterSlices; ++s2)
+            if (md[s2][t] < d) {  // strict: the lower slice keeps a tie
+                d = md[s2][t];
+                i = mi[s2][t];
+            }
+        if (node < nq) values[(long)m * nq + node] = i >= 0 ? cells[3 * cs + a + i] : 0.0;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_raster_stats(const double *__restrict__ values, int nmodels, int nq,
@@ -218,7 +274,8 @@ extern "C" int td_rasterize(td_ctx *ctx, int64_t nmodels, const int64_t *cell_of
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
     // a section's few nodes: every model in one brute-force launch; many nodes: per model,
     // the evaluate path's search (the bucket grid from kGridMinCells cells)
-    const bool batched = nq * (total / std::max<int64_t>(nmodels, 1)) <= (int64_t)1 << 28 && nmodels <= 65535;
+    const bool batched = nq * (total / std::max<int64_t>(nmodels, 1)) <= (int64_t)1 << 28 &&
+                         (int64_t)kXcds * ((nmodels + kXcds - 1) / kXcds) * ((nq + kRasterNodes - 1) / kRasterNodes) <= INT32_MAX;
     if (batched) {
         if (nmodels + 1 > ctx->raster_off_cap) {
             if (ctx->raster_off) (void)hipFree(ctx->raster_off);
@@ -230,8 +287,10 @@ extern "C" int td_rasterize(td_ctx *ctx, int64_t nmodels, const int64_t *cell_of
         TD_HIP(ctx, hipMemcpyAsync(ctx->raster_off, cell_off, sizeof(int64_t) * (size_t)(nmodels + 1),
                                    hipMemcpyHostToDevice, ctx->stream));
         hipEvent_t t0 = tm ? tm->begin(ctx->stream) : nullptr;
-        hipLaunchKernelGGL(k_raster_brute, dim3((unsigned)((nq + kRasterThreads - 1) / kRasterThreads), (unsigned)nmodels),
-                           dim3(kRasterThreads), 0, ctx->stream, ctx->raster_off, dc, cs, dq, (int)nq, dv);
+        const int nchunks = (int)((nq + kRasterNodes - 1) / kRasterNodes);
+        const int64_t blocks = (int64_t)kXcds * ((nmodels + kXcds - 1) / kXcds) * nchunks;
+        hipLaunchKernelGGL(k_raster_brute, dim3((unsigned)blocks), dim3(kRasterThreads), 0, ctx->stream,
+                           ctx->raster_off, dc, cs, dq, (int)nq, (int)nmodels, nchunks, dv);
         if (tm) tm->end("raster_brute", t0, ctx->stream);
         TD_HIP(ctx, hipGetLastError());
     }

@@ -20,6 +20,8 @@ ROWS = {  # traffic.json key -> (run, kernel name)
     "k_nn_grid/config3": ("single", "k_nn_grid"),
     "k_chain_run/stress": ("stress", "k_chain_run<false, false>"),
     "k_nn_grid4/stress": ("stress", "k_nn_grid4"),
+    "k_nn_tile/stress": ("stress", "k_nn_tile<2>"),
+    "k_raster_brute/section": ("aux", "k_raster_brute"),
 }
 
 

@@ -266,11 +266,12 @@ def test_many_rays_exact_chi2(tt, orc, ncells):
     ctx.close()
 
 
-@pytest.mark.parametrize("npts", [1, 5, 255, 257, 3001, 16845, 70000, 133000])
+@pytest.mark.parametrize("npts", [1, 5, 255, 257, 3001, 16845, 70000, 133000, 600000])
 def test_tile_brute_force_plans(tt, orc, ctx, npts):
     """The one-launch brute force (k_nn_tile) over the shapes its plan takes:
     one point per CU (256 slices), a few points per CU, a full config-3 point
-    set, and a point set past its lane budget (the split search takes over);
+    set, and point sets of several tiles per CU (133k: 3 tiles of 174 points;
+    600k, the stress geometry's size: 3 tiles of 782 points in 2 slices);
     cell counts below one group of 8, on and off slice / round boundaries,
     exact ties across slices (duplicated cells) and NaN cells.  Index and
     value must equal the oracle's v_nearest and the split search."""
@@ -279,7 +280,7 @@ def test_tile_brute_force_plans(tt, orc, ctx, npts):
     X = rng.uniform(xmin, xmax, npts)
     Y = rng.uniform(ymin, ymax, npts)
     Z = rng.uniform(zmin, zmax, npts)
-    for nc in ((1, 7, 8, 9, 333, 1023, 5000) if npts <= 16845 else (5000,)):
+    for nc in ((1, 7, 8, 9, 333, 1023, 5000) if npts <= 16845 else (5000,) if npts < 500000 else (2000,)):
         x, y, z, zeta = (a.copy() for a in tt.random_model(nc, nc + 3).cells())
         if nc >= 9:  # duplicates far apart in index (different slices), different values
             k = nc // 3

@@ -64,10 +64,12 @@ def test_plot_model_hist_sections(tt, ds):
 
 
 def test_batched_search_ties_nan_and_chunks(tt, ctx):
-    """A section's nodes take the all-models launch (k_raster_brute): cells
-    staged in 2048-cell chunks, so duplicated cells far apart in index (ties
-    across chunks: the lower index wins), NaN cells, an empty model, cells
-    beyond the 1e9 sentinel distance and nodes on cell sites."""
+    """A section's nodes take the all-models launch (k_raster_brute): a
+    model's cells are split over 8 waves (slices of 625 at 5000 cells), so
+    duplicated cells far apart in index (ties across slices: the lower index
+    wins), NaN cells, an empty model, models of fewer cells than slices x 8,
+    cells beyond the 1e9 sentinel distance and nodes on cell sites; 6 models,
+    not a multiple of the 8 XCDs the models are dealt over."""
     rng = np.random.default_rng(5)
     base = tt.random_model(5000, 55).cells()
     x, y, z, ze = (a.copy() for a in base)
@@ -80,7 +82,8 @@ def test_batched_search_ties_nan_and_chunks(tt, ctx):
     qy = np.concatenate([rng.uniform(-200, 500, 500), y[100:300]])
     qz = np.concatenate([rng.uniform(-10, 700, 500), z[100:300]])
     qx[::50] = np.nan
-    check(ctx, [(x, y, z, ze), far, empty, base, tt.random_model(2048, 9).cells(), tt.random_model(2049, 10).cells()],
+    check(ctx, [(x, y, z, ze), far, empty, base, tt.random_model(2048, 9).cells(), tt.random_model(2049, 10).cells(),
+               tt.random_model(3, 11).cells(), tt.random_model(37, 12).cells()],
           qx, qy, qz)
 
 
