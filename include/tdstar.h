@@ -276,6 +276,26 @@ int td_rounds_create(td_rounds **out, td_chain *const *chains, int64_t nchains);
 int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out);
 int td_rounds_destroy(td_rounds *r);
 
+/* The swap step of parallel tempering (replaces mcmc-in-tonga_amd/tempering.py
+ * decide_swaps, the same decision bit for bit): R replicas, phis[g] and
+ * levels[g] of replica g (gathered over all ranks), temps[l] the ladder.  In
+ * round rnd the level pairs (l, l+1), l = rnd mod 2, 2 + rnd mod 2, ... are
+ * tried with u = a SplitMix64 hash of (seed, rnd, l) and accepted when
+ * log alpha = (phi_a - phi_b)(1/(2T_l) - 1/(2T_l+1)) >= 0 or log u < log alpha
+ * (a at level l, b at l+1).  new_levels[R]; tried/accepted[R-1] are added to
+ * (per level pair).  Host-only (no GPU). */
+int td_swap_decide(int64_t R, const double *phis, const int64_t *levels, const double *temps, int64_t rnd,
+                   uint64_t seed, int64_t *new_levels, int64_t *tried, int64_t *accepted);
+/* M rounds of a resident tempering launch whose replicas are all its chains
+ * (one process, one GPU: the gather is the identity), the swaps decided
+ * between rounds by td_swap_decide -- no return to the caller per round.
+ * Round j: K proposals on every chain at temps[levels[k]] (chain k = replica
+ * k), then the swap step of round rnd0 + j.  levels[nchains] in/out;
+ * phis_out[M x nchains] the phis of each round, levels_out[M x nchains] the
+ * levels after it (both nullable); tried/accepted[nchains - 1] added to. */
+int td_rounds_temper(td_rounds *r, int64_t M, int64_t K, const double *temps, int64_t *levels, int64_t rnd0,
+                     uint64_t seed, double *phis_out, int64_t *levels_out, int64_t *tried, int64_t *accepted);
+
 #ifdef __cplusplus
 }
 #endif

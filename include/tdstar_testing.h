@@ -45,7 +45,6 @@ int tdt_chain_lds(td_chain *ch, int64_t out[4]);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);
-
 /* Device engine layout: 0 (default) mirrors tiles, rays and the Julia order
  * in LDS when they fit (the 381-ray configs); 1 keeps them in HBM, the path
  * larger geometries take.  Same results either way. */

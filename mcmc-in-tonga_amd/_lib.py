@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtdstar.so")
+# (TD_LIB_PATH: a diagnostic A/B of two builds on one box, tools/ only; the product loads the in-tree build)
+LIB_PATH = os.environ.get("TD_LIB_PATH") or os.path.join(HERE, "libtdstar.so")
 
 TD_OK, TD_ERR_ARG, TD_ERR_LAYOUT, TD_ERR_HIP, TD_ERR_NOMEM, TD_ERR_BOUNDS = range(6)
 TD_ENGINE_DEVICE, TD_ENGINE_HOST, TD_ENGINE_DROPIN = 0, 1, 2
@@ -57,6 +58,9 @@ SIGNATURES = {
     "td_rounds_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _i64]),
     "td_rounds_run": (ctypes.c_int, [_vp, _i64, _pd, _pd]),
     "td_rounds_destroy": (ctypes.c_int, [_vp]),
+    "td_swap_decide": (ctypes.c_int, [_i64, _pd, _pi64, _pd, _i64, ctypes.c_uint64, _pi64, _pi64, _pi64]),
+    "td_rounds_temper": (ctypes.c_int, [_vp, _i64, _i64, _pd, _pi64, _i64, ctypes.c_uint64, _pd, _pi64, _pi64,
+                                        _pi64]),
     "td_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "td_timing_reset": (ctypes.c_int, [_vp]),
     "td_timing_get": (ctypes.c_int, [_vp, ctypes.c_char_p, _pi64, _pd]),

@@ -733,6 +733,69 @@ int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out)
     return TD_OK;
 }
 
+namespace {
+// tempering.py _mix64 / _uniform: SplitMix64's finaliser over (seed, round, level)
+uint64_t swap_mix64(uint64_t x) {
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+double swap_uniform(uint64_t seed, uint64_t rnd, uint64_t level) {
+    uint64_t x = swap_mix64(seed * 0x9E3779B97F4A7C15ull + rnd);
+    x = swap_mix64(x + level * 0xD1B54A32D192ED03ull + 1ull);
+    return ((double)(x >> 12) + 0.5) / 4503599627370496.0;  // (k + 1/2) / 2^52: in (0, 1), exact
+}
+}  // namespace
+
+int td_swap_decide(int64_t R, const double *phis, const int64_t *levels, const double *temps, int64_t rnd,
+                   uint64_t seed, int64_t *new_levels, int64_t *tried, int64_t *accepted) {
+    if (R < 1 || !phis || !levels || !temps || !new_levels || rnd < 0) return TD_ERR_ARG;
+    std::vector<int64_t> owner((size_t)R, -1);
+    for (int64_t g = 0; g < R; ++g) {
+        if (levels[g] < 0 || levels[g] >= R || owner[(size_t)levels[g]] >= 0) return TD_ERR_ARG;  // a permutation
+        owner[(size_t)levels[g]] = g;
+        new_levels[g] = levels[g];
+    }
+    for (int64_t l = rnd % 2; l < R - 1; l += 2) {
+        const int64_t a = owner[(size_t)l], b = owner[(size_t)l + 1];
+        if (tried) tried[l] += 1;
+        // tempering.py swap_log_alpha, the same operations (no contraction: -ffp-contract=off)
+        const double la = (phis[a] - phis[b]) * (1.0 / (2.0 * temps[l]) - 1.0 / (2.0 * temps[l + 1]));
+        const double u = swap_uniform(seed, (uint64_t)rnd, (uint64_t)l);
+        if (la >= 0.0 || (u > 0.0 && std::log(u) < la)) {  // (the host libm log, as Python's math.log)
+            new_levels[a] = l + 1;
+            new_levels[b] = l;
+            owner[(size_t)l] = b;
+            owner[(size_t)l + 1] = a;
+            if (accepted) accepted[l] += 1;
+        }
+    }
+    return TD_OK;
+}
+
+int td_rounds_temper(td_rounds *r, int64_t M, int64_t K, const double *temps, int64_t *levels, int64_t rnd0,
+                     uint64_t seed, double *phis_out, int64_t *levels_out, int64_t *tried, int64_t *accepted) {
+    if (!r || M < 0 || K <= 0 || !temps || !levels || rnd0 < 0)
+        return set_err(r ? r->ctx : nullptr, TD_ERR_ARG, "td_rounds_temper");
+    const int64_t R = (int64_t)r->chains.size();
+    std::vector<double> T((size_t)R), phi((size_t)R);
+    std::vector<int64_t> nl((size_t)R);
+    for (int64_t j = 0; j < M; ++j) {
+        for (int64_t k = 0; k < R; ++k) {
+            if (levels[k] < 0 || levels[k] >= R) return set_err(r->ctx, TD_ERR_ARG, "td_rounds_temper: levels");
+            T[(size_t)k] = temps[levels[k]];
+        }
+        const int rc = td_rounds_run(r, K, T.data(), phi.data());
+        if (rc) return rc;
+        if (td_swap_decide(R, phi.data(), levels, temps, rnd0 + j, seed, nl.data(), tried, accepted))
+            return set_err(r->ctx, TD_ERR_ARG, "td_rounds_temper: levels are not a permutation");
+        for (int64_t k = 0; k < R; ++k) levels[k] = nl[(size_t)k];
+        if (phis_out) std::memcpy(phis_out + j * R, phi.data(), sizeof(double) * (size_t)R);
+        if (levels_out) std::memcpy(levels_out + j * R, levels, sizeof(int64_t) * (size_t)R);
+    }
+    return TD_OK;
+}
+
 int td_rounds_destroy(td_rounds *r) {
     if (!r) return TD_OK;
     int rc = rounds_stop(r);
@@ -1222,5 +1285,6 @@ int tdt_accept(const td_chain_params *prm, int action, double u_accept, double z
     tdchain::log_window(lnN, ncells);
     return tdchain::accept(P, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN) ? 1 : 0;
 }
+
 
 }  // extern "C"

@@ -51,6 +51,9 @@ constexpr int kOrphanLds = 256; // orphan records kept in LDS (more: read back f
 constexpr int kPre = 64 / kTilePts;  // LDS layout: hit tiles per wave whose points phase B preloads
 static_assert(kPre == 4, "the preload slots are four registers");
 constexpr int kListLds = 1024;  // rays in HBM: hit tiles / changed rays / hit super-tiles kept in LDS
+// Phase C leaves lanes idle (16 per hit tile, ~8 tiles): wave 7 lane 0 forms the decision's
+// phi_n-free parts; wave 6 lane 0 (LDS layout) begins the next proposal's guess -- its global loads
+// fly across the phase barriers until phase F finishes it there
 // The LDS layout could sum chi^2 with the event walk too; its tails are ~60 terms and the
 // one-wave binade scan with the early-rejection bound is faster there (measured: the walk
 // costs ~1.2k more cycles per proposal at 381 rays x 5000 cells)
@@ -96,28 +99,57 @@ struct PState {
 // TD_inversion_function.jl:72-80,127-128,184-188,221-232: the proposal of one
 // iteration from its draws and the model.  slot_at(pos) = slot at Julia
 // position pos.
+// In two halves: the draws' proposal and the loads of what it needs from the
+// model (the selected cell, or the slot a birth takes), then the rest -- so the
+// loads of a guessed next proposal can fly while other work runs.
+struct ProposalLoads {
+    Proposal q;
+    int s, new_slot;
+    double x, y, z, ze;
+};
+template <class SlotAt>
+__device__ __forceinline__ ProposalLoads proposal_begin(const tdchain::Params &P, const tdchain::Draws &dr,
+                                                        int ncells, int nfree, int nslots, const int *free_slots,
+                                                        const double *cx, const double *cy, const double *cz,
+                                                        const double *czeta, SlotAt slot_at) {
+    ProposalLoads l;
+    l.q = tdchain::propose(P, dr, ncells);
+    l.s = -1;
+    l.new_slot = -1;
+    l.x = l.y = l.z = l.ze = 0.0;
+    if (l.q.active && l.q.action != tdchain::kBirth) {  // (global loads: no LDS wait or barrier waits for them)
+        l.s = slot_at((int)l.q.index);
+        l.x = gload(cx + l.s);
+        l.y = gload(cy + l.s);
+        l.z = gload(cz + l.s);
+        l.ze = gload(czeta + l.s);
+    }
+    if (l.q.active && l.q.action == tdchain::kBirth) l.new_slot = nfree > 0 ? gload(free_slots + nfree - 1) : nslots;
+    return l;
+}
+__device__ __forceinline__ void proposal_end(PState &o, const tdchain::Params &P, const tdchain::Draws &dr,
+                                             ProposalLoads l) {
+    Proposal q = l.q;
+    o.slot_k = -1;
+    o.new_slot = l.new_slot;
+    if (q.active && q.action != tdchain::kBirth) {
+        o.slot_k = l.s;
+        o.kx = l.x;
+        o.ky = l.y;
+        o.kz = l.z;
+        o.zeta_killed = l.ze;
+        tdchain::complete_proposal(P, dr, q, l.x, l.y, l.z, l.ze);
+    }
+    o.p = q;
+    // forward evaluation needed (birth validity is only known after its query)
+    o.eval = q.active && (q.valid || q.action == tdchain::kBirth) && P.debug_prior != 1;
+}
 template <class SlotAt>
 __device__ __forceinline__ void make_proposal(PState &o, const tdchain::Params &P, const tdchain::Draws &dr,
                                               int ncells, int nfree, int nslots, const int *free_slots,
                                               const double *cx, const double *cy, const double *cz,
                                               const double *czeta, SlotAt slot_at) {
-    Proposal q = tdchain::propose(P, dr, ncells);
-    o.slot_k = -1;
-    o.new_slot = -1;
-    if (q.active && q.action != tdchain::kBirth) {
-        const int s = slot_at((int)q.index);
-        const double x = cx[s], y = cy[s], z = cz[s], ze = czeta[s];
-        o.slot_k = s;
-        o.kx = x;
-        o.ky = y;
-        o.kz = z;
-        o.zeta_killed = ze;
-        tdchain::complete_proposal(P, dr, q, x, y, z, ze);
-    }
-    if (q.active && q.action == tdchain::kBirth) o.new_slot = nfree > 0 ? free_slots[nfree - 1] : nslots;
-    o.p = q;
-    // forward evaluation needed (birth validity is only known after its query)
-    o.eval = q.active && (q.valid || q.action == tdchain::kBirth) && P.debug_prior != 1;
+    proposal_end(o, P, dr, proposal_begin(P, dr, ncells, nfree, nslots, free_slots, cx, cy, cz, czeta, slot_at));
 }
 
 // A scripted step (td_evaluate's incremental path) as the proposal: always
@@ -161,8 +193,13 @@ __device__ __forceinline__ void script_proposal(PState &o, const ScriptStep &st,
 struct Shared {
     PState ps[2];      // this iteration's proposal (ps[cur]) and the next one guessed in phase F
     int cur, spec_ok;
-    int early_reject;  // phase F: the decision is "reject" whatever the remaining chi^2 terms
+    int defer;  // phase F: accepted on bounds (LDS layout): the new chi^2 partial sums are not formed
     double phi_n;
+    // decisions on bounds (phase F; wave 0): prefix[] exact below ex_upto, phi_r an
+    // estimate in [phi_lo, phi_hi] (held here, not in registers: the kernel is at its VGPR limit)
+    int ex_upto;
+    double phi_lo, phi_hi, b_lo, b_hi;
+    double wpart[kChainThreads / 64];  // rays in HBM: each wave's part of the any-order sum of the terms
     int accept;
     int n_tiles, n_changed, n_orphans, n_rays, k0;
     int n_super[2];  // rays in HBM: super-tiles hit, by iteration parity (the next iteration refreshes their maxima)
@@ -728,6 +765,42 @@ struct CopySeg {
     }
 };
 
+// LDS layout, one wave (the rare paths of the decisions on bounds, phase F):
+// prefix[ex_upto..n) exact again -- the committed terms added in k order
+// (MCsub.jl:170-172, exact_sum.h) -- and the committed phi returned; then, if
+// k0 < n, the proposal's partial sums from k0 into cprefix, its phi_n in
+// *phi_n.  `overlay`: a proposal's terms are in place (its rays flagged, their
+// committed terms in cterm), staged through cprefix.  Out of line: it is
+// rare, and the kernel is at its register limit.
+// (The arrays by value: a Views passed by reference would be spilled to scratch in the caller.)
+__device__ __attribute__((noinline)) double exact_sums(const double *term, double *prefix, double *cprefix,
+                                                       const double *cterm, const int *rflag, Shared &sh, int n,
+                                                       int lane, bool overlay, int k0, double phi, double *phi_n) {
+    const int ex_upto = sh.ex_upto;
+    if (ex_upto < n) {
+        const double C0 = ex_upto > 0 ? prefix[ex_upto - 1] : 0.0;
+        const double *t = term + ex_upto;
+        if (overlay) {
+            for (int k = ex_upto + lane; k < n; k += 64) cprefix[k] = rflag[k] ? cterm[k] : term[k];
+            wave_sync_lds();
+            t = cprefix + ex_upto;
+        }
+        bool stopped = false;
+        phi = wave_seq_sum(t, n - ex_upto, C0, prefix + ex_upto, lane, nullptr, &stopped);
+        wave_sync_lds();
+        if (lane == 0) {
+            sh.ex_upto = n;
+            sh.phi_lo = sh.phi_hi = phi;
+        }
+        wave_sync_lds();
+    }
+    if (k0 < n) {
+        bool stopped = false;
+        *phi_n = wave_seq_sum(term + k0, n - k0, k0 > 0 ? prefix[k0 - 1] : 0.0, cprefix + k0, lane, nullptr, &stopped);
+    }
+    return phi;
+}
+
 // SCRIPT: host-given proposals (td_evaluate's incremental path: scripted
 // steps, the resident server); a free-running chain's instance has none of
 // that code on its path.
@@ -825,7 +898,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.evaluations = 0;
         sh.bytes = 0;
         sh.cur = 0;
-        sh.early_reject = 0;
+        sh.defer = 0;
         sh.grid_fallbacks32 = 0;
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
@@ -932,6 +1005,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     bool pend_sup = false;  // rays in HBM: its super-tiles' maxima not yet refreshed
     int last_action = 0, last_accept = 0;  // tid 0: Model.action / accept of the last iteration
     long long it_done = 0;                 // iterations run (server mode: until QUIT)
+    // LDS layout, decisions on bounds (phase F): a proposal accepted on bounds of phi_n leaves its
+    // chi^2 partial sums unformed -- prefix[] stays exact below ex_upto only (wave 0), and tid 0
+    // keeps phi_r as an estimate inside [phi_lo, phi_hi].  They are made exact again by the next
+    // decision the bounds cannot take, at a tempering round's end and at the launch's end.
+    if (tid == 0) {
+        sh.ex_upto = n;
+        sh.phi_lo = sh.phi_hi = phi_r;
+    }
+    __syncthreads();
     for (long long it = 0; it < iters && !((mb || rbx) && sh.srv_quit); ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
         // rays in HBM: the previous accepted proposal's super-tile maxima (their first round of
@@ -1154,6 +1236,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             int no = 0;
             if (fwd) {
                 // ================= phase C: affected points =================
+
                 const int nt = sh.n_tiles;
                 // the selected cell's Julia position and value, known since the proposal was made:
                 // rank[slot_k] = p.index (slot_k = ord[p.index]), czeta[slot_k] = zeta_killed (no load)
@@ -1293,53 +1376,120 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         v.cterm[r] = old_term;                       // kept to undo a rejection
                         v.term[r] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                         atomicAdd(&sh.ray_pts, npr);
-                        if constexpr (WALK) atomicOr(&cmask[r >> 6], 1ull << (r & 63));  // an event of the walk
+                        if constexpr (WALK)  // an event of the walk (scripted steps: the decisions on bounds need none)
+                            if (nscript) atomicOr(&cmask[r >> 6], 1ull << (r & 63));
                     }
                 }
                 __syncthreads();
                 STAMP(4);
             }
-            // ==== phase F: chi^2 + decision (tid 0) || next proposal, tile maxima (others) ====
+            // ==== phase F: chi^2 + decision (wave 0) || next proposal, tile maxima (rays in HBM) ====
             const long long tF = prof_on ? clock64() : 0;  // diagnostic: per-wave time in F
+            constexpr bool spec_in_F = true;
             double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
+            int bdec = 0;        // wave 0, LDS layout: 1 rejected / 2 accepted on bounds, 0 on the exact phi_n
+            if constexpr (WALK) {
+                // rays in HBM, decisions on bounds (below): the whole block adds the proposal's
+                // terms in any order -- n / 512 global loads per thread, four in flight
+                if (!nscript && fwd && sh.k0 < n) {  // (block-uniform)
+                    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+                    int k = tid;
+                    for (; k + 3 * kChainThreads < n; k += 4 * kChainThreads) {
+                        p0 = p0 + gload(v.term + k);
+                        p1 = p1 + gload(v.term + k + kChainThreads);
+                        p2 = p2 + gload(v.term + k + 2 * kChainThreads);
+                        p3 = p3 + gload(v.term + k + 3 * kChainThreads);
+                    }
+                    for (; k < n; k += kChainThreads) p0 = p0 + gload(v.term + k);
+                    const double wsum = wave_sum_f64((p0 + p1) + (p2 + p3));
+                    if (lane == 0) sh.wpart[wv] = wsum;
+                    __syncthreads();
+                }
+            }
             if (wv == 0) {
                 const int k0 = sh.k0;
                 if (fwd) {
                     // the terms added in k order (MCsub.jl:170-172), bit for bit, by this
                     // wave (exact_sum.h); phase E put the changed rays' new terms in place
-                    // (the old ones wait in cterm, their sums in prefix).  Rays in LDS:
-                    // binade-run scans of the tail, and the last wave may prove meanwhile
-                    // that no remaining sum can be accepted (sh.early_reject): the sum
-                    // stops.  Rays in HBM (long tails, few changed terms): the new sums
-                    // follow the old ones at a checked constant offset between events.
-                    double C = k0 > 0 ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
-                    if (k0 < n) {
-                        bool stopped = false;
-                        long long *rc = prof_on && !WALK ? &sh.prof[65] : nullptr;
-                        if constexpr (!WALK)
-                            C = wave_seq_sum(v.term + k0, n - k0, C, v.cprefix + k0, lane, &sh.early_reject, &stopped,
-                                             rc);
-                        else  // O(events), not O(tail): exact_sum.h delta_walk
+                    // (the old ones wait in cterm, their sums in prefix).
+                    // Rays in LDS: the decision first, on bounds.  The terms are >= 0, so
+                    // their sequential sum is within n ulps of any other association: the
+                    // sum of ALL the proposal's terms in any order (one DPP reduction,
+                    // whatever k0) brackets phi_n within 1e-9; phi_r is exact or likewise
+                    // bracketed; the decision is monotone (up in phi, down in phi_n), so
+                    // when it is the same at both corners of the brackets it is the one the
+                    // exact values give.  A rejection then needs no exact sum; an acceptance
+                    // leaves its partial sums unformed (prefix exact below ex_upto, phi_r an
+                    // estimate in [phi_lo, phi_hi]) until a decision the brackets cannot
+                    // take (phi_n within ~1e-9 of the threshold), a tempering round's end or
+                    // the launch's end: then the committed terms from ex_upto and the
+                    // proposal's from k0 are added in order, the binade-run scans.
+                    // Rays in HBM: the same, the sum of all terms formed by the whole block
+                    // (above); a scripted step (exact every time) walks the events instead --
+                    // the new sums follow the old ones at a checked constant offset between
+                    // events (exact_sum.h delta_walk).
+                    if (!WALK || !nscript) {
+                        // nothing changed (k0 == n): phi_n IS phi_r, estimate or not (MCsub.jl:169-172
+                        // adds the same terms), and phi - phi_n = 0 in the decision either way
+                        bool exact = nscript != 0;
+                        if (k0 >= n) phi_n = phi_r;
+                        if (!exact && k0 < n) {
+                            double Sa = 0.0;
+                            if constexpr (WALK) {
+                                for (int w = 0; w < kWaves; ++w) Sa = Sa + sh.wpart[w];
+                            } else {
+                                double part = 0.0;
+                                for (int k = lane; k < n; k += 64) part = part + v.term[k];
+                                Sa = wave_sum_f64(part);
+                            }
+                            const double b_lo = Sa * (1.0 - 1e-9), b_hi = Sa * (1.0 + 1e-9);
+                            if (lane == 0) {
+                                const bool a_min = tdchain::accept_t(P, inv2t_r, pp, sh.phi_lo, b_hi, czeta, zeta_killed,
+                                                                     zetanew_death, sh.lnN);
+                                const bool a_max = tdchain::accept_t(P, inv2t_r, pp, sh.phi_hi, b_lo, czeta, zeta_killed,
+                                                                     zetanew_death, sh.lnN);
+                                bdec = a_min != a_max ? 0 : a_min ? 2 : 1;
+                            }
+                            bdec = __builtin_amdgcn_readfirstlane(bdec);
+                            // a tempering round's last iteration publishes phi: decided exactly (and
+                            // every sum made exact) whatever the bounds say
+                            if (rbx && it + 1 == round_end) bdec = 0;
+                            exact = bdec == 0;
+                            phi_n = Sa;  // (an estimate on a decided proposal)
+                            if (bdec == 2 && lane == 0) {  // the accepted terms' sums: unformed
+                                sh.ex_upto = min(sh.ex_upto, k0);
+                                sh.b_lo = b_lo;
+                                sh.b_hi = b_hi;
+                            }
+                        }
+                        if (exact && k0 < n) {  // the committed partial sums and phi_r, then the proposal's
+                            phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, true, k0, phi_r, &phi_n);
+                            if (prof_on && lane == 0) sh.prof[65] += 1;  // (diagnostic: exact decisions)
+                        }
+                        if (prof_on && lane == 0 && k0 < n) sh.prof[64] += n - k0;
+                    } else {
+                        double C = k0 > 0 ? v.prefix[k0 - 1] : 0.0;  // MCsub.jl:169 C = 0
+                        if (k0 < n) {  // O(events), not O(tail): exact_sum.h delta_walk
                             C = delta_walk(v.term, v.prefix, v.rflag, k0, n, C, smask, cmask, v.cprefix, sh.dseg, lane,
                                            prof_on ? &sh.prof[72] : nullptr);
-                        if (prof_on && lane == 0) sh.prof[64] += n - k0;
+                            if (prof_on && lane == 0) sh.prof[64] += n - k0;
+                        }
+                        phi_n = k0 < n ? C : sh.phi;
                     }
-                    phi_n = k0 < n ? C : sh.phi;
                 }
                 if (prof_on && lane == 0) sh.prof[66] += clock64() - tF;  // diagnostic: scan done
             }
             if (tid == 0) {
-                const int k0 = sh.k0;
-                // Metropolis-Hastings decision (a proven rejection skips the rest of the sum:
-                // accept() on the exact phi_n would reject too)
-                const bool early = fwd && k0 < n && sh.early_reject;
+                // Metropolis-Hastings decision (on bounds: the one accept() gives on the exact values);
                 // a scripted step's decision is given (kDecideLater: by the server's next command;
                 // the grid update below is then staged and applied only if it is a commit)
                 const bool acc = nscript ? sh.step_cur.decision == 1
-                                         : !early && tdchain::accept_t(P, inv2t_r, pp, phi_r, phi_n, czeta,
-                                                                       zeta_killed, zetanew_death, sh.lnN);
+                                 : bdec != 0 ? bdec == 2
+                                             : tdchain::accept_t(P, inv2t_r, pp, phi_r, phi_n, czeta, zeta_killed,
+                                                                 zetanew_death, sh.lnN);
                 acc_r = acc;
                 sh.accept = acc ? 1 : 0;
+                sh.defer = bdec == 2 ? 1 : 0;
                 sh.phi_n = phi_n;
                 if (prof_on) sh.prof[67] += clock64() - tF;  // diagnostic: decision taken
                 if (acc || (mb && sh.step_cur.decision == kDecideLater)) {
@@ -1354,8 +1504,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.g_nz = pp.z;
                     if (acc) atomicAdd((unsigned long long *)&sh.accepted[action], 1ull);
                 }
-                if (prof_on && early) atomicAdd((unsigned long long *)&sh.prof[14], 1ull);  // proven rejections
-            } else if (tid == 64) {  // the next proposal as if this one were rejected
+                if (prof_on && bdec == 1) atomicAdd((unsigned long long *)&sh.prof[14], 1ull);  // rejected on bounds
+            } else if (spec_in_F && tid == 64) {  // the next proposal as if this one were rejected
                 if (can_spec) {
                     make_proposal(sh.ps[sh.cur ^ 1], P, draws[(it + 1) & 63], ncells, sh.nfree, sh.nslots, d.free_slots, d.cx,
                                   d.cy, d.cz, d.czeta, [&](int pos) { return v.ord[pos]; });
@@ -1390,25 +1540,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.lnN_far[0] = d.logN[max(ncells - 2, 0)];
                     sh.lnN_far[1] = d.logN[ncells + 2];
                 }
-                // a lower bound of phi_n from all new terms: the sequential sum of n
-                // non-negative terms is within n ulps of any other association; above
-                // the rejection bound by a wide margin, the proposal is rejected
-                const int k0 = sh.k0;
-                if (!WALK && fwd && k0 < n && !nscript) {
-                    // the bound first: it does not depend on the sum (computed while the terms load)
-                    const double thr = tdchain::reject_bound_t(P, sh.rT, sh.rinv2t, pp, sh.phi, czeta, zeta_killed,
-                                                               zetanew_death, sh.lnN);
-                    const double C0 = k0 > 0 ? v.prefix[k0 - 1] : 0.0;
-                    double part = 0.0;
-                    for (int k = k0 + lane; k < n; k += 64) part = part + v.term[k];
-                    const double S = wave_sum_f64(part);
-                    if (lane == 0) {
-                        const double lb = (C0 + S) * (1.0 - 1e-9);
-                        if (lb > thr + 1e-7 * (fabs(thr) + fabs(sh.phi)) + 1e-6)
-                            __hip_atomic_store(&sh.early_reject, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-            } else if (wv >= 2 && fwd && action != tdchain::kChange) {
+            } else if (wv >= 2 && wv <= kWaves - 3 && fwd && action != tdchain::kChange) {  // waves 2..5
                 // the hit tiles' maxima if the proposal is accepted (a tile = a DPP row)
                 const int nt = sh.n_tiles;
                 for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 256) {
@@ -1483,8 +1615,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     v.ptS[r] = v.cptS[r];
                     v.rflag[r] = 0;
                 }
-                if constexpr (!WALK) {
-                    for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
+                if (!WALK || !nscript) {
+                    if (!sh.defer)  // (accepted on bounds: its partial sums are left unformed)
+                        for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
                 } else if (fwd && k0 < n) {
                     pend_r = true;  // written at the top of the next iteration
                     if (wv == 1) delta_remark(v.term, v.prefix, v.cprefix, n, sh.dseg, smask, lane);
@@ -1541,8 +1674,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         d.cy[sk] = pp.y;
                         d.cz[sk] = pp.z;
                     }
-                    phi_r = sh.phi_n;
-                    sh.phi = phi_r;
+                    if (bdec == 2) {  // an estimate inside the bracket of phase F
+                        phi_r = sh.phi_n;
+                        sh.phi_lo = sh.b_lo;
+                        sh.phi_hi = sh.b_hi;
+                    } else if (!(!nscript && fwd && sh.k0 >= n)) {  // (nothing changed: phi_r stays)
+                        phi_r = sh.phi_n;
+                        sh.phi_lo = sh.phi_hi = phi_r;
+                        sh.phi = phi_r;
+                    }
                 }
             } else {  // rejected: flags down, the changed rays get their old chi^2 terms back
                 if (wv != 0)
@@ -1561,6 +1701,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         if (wv == 0) {
             if (prof_on && lane == 0) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
             if (rbx && it + 1 == round_end) {  // a tempering round is done: publish phi, take the next temperature
+                {  // (a phase F of this iteration made every sum exact already)
+                    double unused = 0.0;
+                    phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, false, n, phi_r, &unused);
+                    if (lane == 0) sh.phi = phi_r;
+                }
                 round_wait(rbx, bchain, sh, lane, true, phi_r);  // (lane 0 = tid 0 holds phi)
                 inv2t_r = sh.rinv2t;
                 round_end = it + 1 + sh.rK;
@@ -1599,7 +1744,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     const tdchain::Proposal &np = sh.ps[cur_r].p;
                     if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
                     sh.spec_ok = 0;
-                    sh.early_reject = 0;
                     sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
                     sh.n_super[(it + 1) & 1] = 0;  // the other parity's list is refreshed first
                     sh.pts_seen = sh.ray_pts = 0;
@@ -1615,6 +1759,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     }
 
     const long long t_loop_end = prof_on ? clock64() : 0;
+    {  // decisions on bounds: the partial sums and phi exact again (the launch leaves them)
+        if (wv == 0) {
+            double unused = 0.0;
+            phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, false, n, phi_r, &unused);
+            if (lane == 0) sh.phi = phi_r;
+        }
+        __syncthreads();
+    }
     if constexpr (WALK) {
         if (pend_r) delta_commit<SMALL ? 1 : 16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
         if constexpr (SMALL) __syncthreads();  // the LDS sums are written back below

@@ -9,6 +9,20 @@
 
 namespace tdstar {
 
+// A load through an address-space-1 (global) pointer: `global_load`, counted in
+// vmcnt only.  The same load through a generic pointer is a `flat_load`, counted
+// in lgkmcnt too -- and every LDS wait and block barrier (which waits on
+// lgkmcnt) would then wait for it.  p must point to device global memory.
+template <class T>
+__device__ __forceinline__ T gload(const T *p) {
+    return *(const __attribute__((address_space(1))) T *)(p);
+}
+
+template <class T>
+__device__ __forceinline__ void gstore(T *p, T v) {
+    *(__attribute__((address_space(1))) T *)(p) = v;
+}
+
 // LDS writes of this wave visible to its own later reads (no block barrier)
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

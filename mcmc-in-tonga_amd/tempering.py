@@ -178,6 +178,45 @@ class TemperingLadder:
         self.rnd += 1
         return allphi
 
+    def run(self, rounds, k):
+        """``rounds`` x ``step(k)``.  One process holding every replica in a
+        resident launch (BASELINE config 4 on one GPU): the rounds and their
+        swap steps run in the library (td_rounds_temper, td_swap_decide: the
+        same decisions as decide_swaps, bit for bit) without a return to
+        Python per round; the trace is the same.  Returns the last gathered phis."""
+        rounds = int(rounds)
+        if not (self.resident and self.ex.world == 1 and rounds > 0):
+            out = None
+            for _ in range(rounds):
+                out = self.step(k)
+            return out
+        import ctypes
+
+        from ._lib import _pi64, check, lib, ptr
+
+        if self.rounds is None:
+            from .chain import Rounds
+
+            self.rounds = Rounds(self.chains)
+        R = self.R
+        phis = np.empty((rounds, R), dtype=np.float64)
+        lv_out = np.empty((rounds, R), dtype=np.int64)
+        levels = np.ascontiguousarray(self.levels, dtype=np.int64).copy()
+        tried = np.zeros(max(R - 1, 1), dtype=np.int64)
+        acc = np.zeros(max(R - 1, 1), dtype=np.int64)
+        temps = np.ascontiguousarray(self.temps, dtype=np.float64)
+        check(lib().td_rounds_temper(self.rounds.h, rounds, int(k), ptr(temps), ptr(levels, _pi64), int(self.rnd),
+                                     ctypes.c_uint64(int(self.seed) & _M64), ptr(phis), ptr(lv_out, _pi64),
+                                     ptr(tried, _pi64), ptr(acc, _pi64)), self.chains[0].ctx.h)
+        for j in range(rounds):
+            self._trace.update(phis[j].tobytes())
+            self._trace.update(lv_out[j].tobytes())
+        self.tried += tried[:R - 1]
+        self.accepted += acc[:R - 1]
+        self.levels = levels
+        self.rnd += rounds
+        return phis[-1].copy()
+
     def close(self):
         """End the resident launch (the chains' counts and models are current after it)."""
         if self.rounds is not None:

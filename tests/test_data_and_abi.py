@@ -265,3 +265,4 @@ def test_acceptance_matches_reference_formulas(tt):
                     continue
                 got = L.tdt_accept(ctypes.byref(prm), action, u, zn, N, phi, phi_n, cz, zk, zd)
                 assert got == (1 if u < a else 0), (prior, action, a, u)
+

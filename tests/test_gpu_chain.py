@@ -303,3 +303,33 @@ def test_resident_rounds_equal_launch_per_round(tt, ds, ctx):
         assert same_models(a, b)
         assert x["phi"] == y["phi"] and x["accepted"] == y["accepted"] and x["proposed"] == y["proposed"]
         assert x["iterations"] == y["iterations"] == 20 * 10 + 10 * 7
+
+
+def test_library_tempering_loop_equals_round_by_round(tt, ds, ctx):
+    """TemperingLadder.run (td_rounds_temper: the resident launch with the swap
+    steps decided in the library between rounds, no return to Python per
+    round) gives exactly the trace, levels, swap counts, models and stats of
+    the same rounds stepped one by one from Python with decide_swaps, in two
+    calls of different round sizes."""
+    prm = tt.define_TDstructrure().replace(max_cells=600)
+    runs = []
+    for native in (True, False):
+        chains = [make(tt, ctx, prm, tt.random_model(250 + 20 * j, 80 + j), 80 + j, tt.TD_ENGINE_DEVICE,
+                       chain=1 + j) for j in range(6)]
+        lad = tt.TemperingLadder(chains, tmax=8.0, seed=7, resident=True)
+        if native:
+            lad.run(25, 10)
+            lad.run(11, 4)
+        else:
+            for r in range(36):
+                lad.step(10 if r < 25 else 4)
+        lad.close()
+        runs.append((lad.trace_digest(), list(lad.levels), list(lad.tried), list(lad.accepted),
+                     [c.model() for c in chains], [c.stats() for c in chains], lad.rnd))
+        for c in chains:
+            c.close()
+    a, b = runs
+    assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2] and a[3] == b[3] and a[6] == b[6] == 36
+    for ma, mb, x, y in zip(a[4], b[4], a[5], b[5]):
+        assert same_models(ma, mb)
+        assert x["phi"] == y["phi"] and x["accepted"] == y["accepted"] and x["proposed"] == y["proposed"]

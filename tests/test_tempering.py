@@ -128,3 +128,44 @@ def test_gloo_world2_matches_single_process(tmp_path):
         assert list(map(float, phis)) == r0["trace"][k][0]
         assert list(map(int, lad.levels)) == r0["trace"][k][1]
     assert [c.T for c in chains] == r0["temps"] + r1["temps"]
+
+
+def test_native_swap_step_is_decide_swaps(tt):
+    """td_swap_decide (the library's swap step, which td_rounds_temper runs
+    between resident rounds) makes decide_swaps' decisions bit for bit: the
+    same SplitMix64 uniforms, the same log alpha, the host libm log -- over
+    random ladders, levels and phis, both round parities, and phis that make
+    log alpha 0, +-inf or NaN."""
+    import ctypes
+
+    from importlib import import_module
+
+    tp = import_module(tt.__name__ + ".tempering")
+    L = tt.lib()
+    rng = np.random.default_rng(5)
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    PD = ctypes.POINTER(ctypes.c_double)
+    for trial in range(3000):
+        R = int(rng.integers(1, 12))
+        temps = tp.geometric_ladder(R, float(rng.uniform(1.5, 20.0)))
+        levels = rng.permutation(R).astype(np.int64)
+        phis = rng.normal(6000.0, float(rng.choice([1.0, 30.0, 3000.0])), R)
+        if trial % 7 == 0 and R > 1:
+            phis[int(rng.integers(0, R))] = (np.inf, -np.inf, np.nan, phis[0])[trial % 4]
+        rnd, seed = int(rng.integers(0, 1 << 40)), int(rng.integers(0, 1 << 62))
+        want, wt, wa = tp.decide_swaps(phis, levels, temps, rnd, seed)
+        got = np.empty(R, dtype=np.int64)
+        t = np.zeros(max(R - 1, 1), dtype=np.int64)
+        a = np.zeros(max(R - 1, 1), dtype=np.int64)
+        rc = L.td_swap_decide(R, phis.ctypes.data_as(PD), levels.ctypes.data_as(P64), temps.ctypes.data_as(PD), rnd,
+                              ctypes.c_uint64(seed), got.ctypes.data_as(P64), t.ctypes.data_as(P64),
+                              a.ctypes.data_as(P64))
+        assert rc == 0
+        assert np.array_equal(got, want), (trial, R, rnd)
+        assert np.array_equal(t[:R - 1], wt) and np.array_equal(a[:R - 1], wa)
+    bad = np.array([0, 0, 1], dtype=np.int64)  # not a permutation: refused
+    out = np.empty(3, dtype=np.int64)
+    ph = np.zeros(3)
+    tl = tp.geometric_ladder(3)
+    assert L.td_swap_decide(3, ph.ctypes.data_as(PD), bad.ctypes.data_as(P64), tl.ctypes.data_as(PD), 0,
+                            ctypes.c_uint64(1), out.ctypes.data_as(P64), None, None) != 0
