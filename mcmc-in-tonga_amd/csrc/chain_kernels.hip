@@ -199,7 +199,6 @@ struct Shared {
     // estimate in [phi_lo, phi_hi] (held here, not in registers: the kernel is at its VGPR limit)
     int ex_upto;
     double phi_lo, phi_hi, b_lo, b_hi;
-    double wpart[kChainThreads / 64];  // rays in HBM: each wave's part of the any-order sum of the terms
     int accept;
     int n_tiles, n_changed, n_orphans, n_rays, k0;
     int n_super[2];  // rays in HBM: super-tiles hit, by iteration parity (the next iteration refreshes their maxima)
@@ -233,6 +232,10 @@ struct Shared {
     OrphanRec orph[kOrphanLds];
     DeltaSegs dseg;  // rays in HBM: phase F's new chi^2 partial sums as segments over the old ones
     long long prof[kProfSlots], t_last, t_iter;  // diagnostic phase stamps
+    // rays in HBM: the committed terms' sum kept in any order, |tsum - (the exact real sum)| <=
+    // terr; a proposal adds dsum = its terms' changes (any order), dabs = their magnitudes (phase E)
+    double tsum, terr, dsum, dabs, b_T, b_E;
+    double wpart[kChainThreads / 64];  // each wave's part of a block-wide any-order sum of the terms
 };
 
 // Diagnostic phase stamp (lane 0 of wave 0, right after a barrier): cycles
@@ -765,6 +768,10 @@ struct CopySeg {
     }
 };
 
+// The decisions on bounds (phase F): 2u, u = 2^-53 the unit roundoff -- every rounding bound below is
+// taken twice over
+constexpr double kSumSlack = 2.3e-16;
+
 // LDS layout, one wave (the rare paths of the decisions on bounds, phase F):
 // prefix[ex_upto..n) exact again -- the committed terms added in k order
 // (MCsub.jl:170-172, exact_sum.h) -- and the committed phi returned; then, if
@@ -887,10 +894,19 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const long long t_mirror = prof_on ? clock64() : 0;
     // chi^2 term of every ray in the current state (MCsub.jl:171), cached: a
     // proposal recomputes only the terms of the rays it changes
-    for (int r = tid; r < n; r += kChainThreads) {
-        const double df = v.ptS[r] - v.tS[r];
-        const double sg = v.sig[r];
-        v.term[r] = ((df * df) * 1.0) / (sg * sg);
+    {
+        double part = 0.0;  // (rays in HBM: their sum in any order, the running total of phase F)
+        for (int r = tid; r < n; r += kChainThreads) {
+            const double df = v.ptS[r] - v.tS[r];
+            const double sg = v.sig[r];
+            const double t = ((df * df) * 1.0) / (sg * sg);
+            v.term[r] = t;
+            part = part + t;
+        }
+        if constexpr (!SMALL) {
+            part = wave_sum_f64(part);
+            if (lane == 0) sh.wpart[wv] = part;
+        }
     }
     if (tid == 0) {
         const ChainScalars &s0 = *d.st;
@@ -899,6 +915,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.bytes = 0;
         sh.cur = 0;
         sh.defer = 0;
+        if (!SMALL) sh.dsum = sh.dabs = 0.0;
         sh.grid_fallbacks32 = 0;
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
@@ -1012,6 +1029,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     if (tid == 0) {
         sh.ex_upto = n;
         sh.phi_lo = sh.phi_hi = phi_r;
+        if constexpr (!SMALL) {
+            double T = 0.0;
+            for (int w = 0; w < kWaves; ++w) T = T + sh.wpart[w];
+            sh.tsum = T;
+            sh.terr = kSumSlack * (double)(n + 1) * fabs(T);  // (any order: within (n - 1) ulps of the exact sum)
+        }
     }
     __syncthreads();
     for (long long it = 0; it < iters && !((mb || rbx) && sh.srv_quit); ++it) {
@@ -1374,7 +1397,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         const double df = val - tsr;
                         const double sg = sgr;
                         v.cterm[r] = old_term;                       // kept to undo a rejection
-                        v.term[r] = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
+                        const double nterm = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
+                        v.term[r] = nterm;
+                        if constexpr (!SMALL) {  // (the running total: any order; rays in LDS re-add them all)
+                            atomicAdd(&sh.dsum, nterm - old_term);
+                            atomicAdd(&sh.dabs, fabs(nterm) + fabs(old_term));
+                        }
                         atomicAdd(&sh.ray_pts, npr);
                         if constexpr (WALK)  // an event of the walk (scripted steps: the decisions on bounds need none)
                             if (nscript) atomicOr(&cmask[r >> 6], 1ull << (r & 63));
@@ -1388,10 +1416,20 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             constexpr bool spec_in_F = true;
             double phi_n = 1.0;  // debug_prior: MCsub.jl:134-136
             int bdec = 0;        // wave 0, LDS layout: 1 rejected / 2 accepted on bounds, 0 on the exact phi_n
+            // The proposal's terms summed in any order (decisions on bounds, below): the committed
+            // running total plus phase E's changes, Tp, within Ep of the exact real sum (every
+            // rounding bounded twice over: the total's own bound, the changes and their magnitudes
+            // added in any order, the one add).  When Ep passes 1e-10 of Tp (or is not finite) the
+            // sum is formed afresh from all the terms (block-uniform: every lane reads the same LDS).
+            // Rays in LDS: the ~400 terms are re-added every time (one wave, one DPP reduction: as
+            // cheap as keeping the total).
+            const double Tp = SMALL ? 0.0 : sh.tsum + sh.dsum;
+            const double Ep = SMALL ? 0.0 : sh.terr + kSumSlack * ((double)(sh.n_rays + 2) * sh.dabs + fabs(Tp));
+            const bool anchor = SMALL || !(Ep <= 1e-10 * Tp);
             if constexpr (WALK) {
-                // rays in HBM, decisions on bounds (below): the whole block adds the proposal's
-                // terms in any order -- n / 512 global loads per thread, four in flight
-                if (!nscript && fwd && sh.k0 < n) {  // (block-uniform)
+                // rays in HBM: the whole block adds the proposal's terms afresh in any order --
+                // n / 512 global loads per thread, four in flight
+                if (!nscript && fwd && sh.k0 < n && anchor) {  // (block-uniform)
                     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
                     int k = tid;
                     for (; k + 3 * kChainThreads < n; k += 4 * kChainThreads) {
@@ -1434,15 +1472,24 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         bool exact = nscript != 0;
                         if (k0 >= n) phi_n = phi_r;
                         if (!exact && k0 < n) {
-                            double Sa = 0.0;
-                            if constexpr (WALK) {
-                                for (int w = 0; w < kWaves; ++w) Sa = Sa + sh.wpart[w];
-                            } else {
-                                double part = 0.0;
-                                for (int k = lane; k < n; k += 64) part = part + v.term[k];
-                                Sa = wave_sum_f64(part);
+                            double Sa = Tp, Ea = Ep;
+                            if (anchor) {
+                                Sa = 0.0;
+                                if constexpr (WALK) {
+                                    for (int w = 0; w < kWaves; ++w) Sa = Sa + sh.wpart[w];
+                                } else {
+                                    double part = 0.0;
+                                    for (int k = lane; k < n; k += 64) part = part + v.term[k];
+                                    Sa = wave_sum_f64(part);
+                                }
+                                Ea = kSumSlack * (double)(n + 1) * fabs(Sa);
                             }
-                            const double b_lo = Sa * (1.0 - 1e-9), b_hi = Sa * (1.0 + 1e-9);
+                            if (!SMALL && lane == 0) {  // the running total if the proposal is committed
+                                sh.b_T = Sa;
+                                sh.b_E = Ea;
+                            }
+                            // the sequential phi_n lies within (n - 1) ulps of the exact sum, far inside 1e-9
+                            const double b_lo = (Sa - Ea) * (1.0 - 1e-9), b_hi = (Sa + Ea) * (1.0 + 1e-9);
                             if (lane == 0) {
                                 const bool a_min = tdchain::accept_t(P, inv2t_r, pp, sh.phi_lo, b_hi, czeta, zeta_killed,
                                                                      zetanew_death, sh.lnN);
@@ -1541,18 +1588,50 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     sh.lnN_far[1] = d.logN[ncells + 2];
                 }
             } else if (wv >= 2 && wv <= kWaves - 3 && fwd && action != tdchain::kChange) {  // waves 2..5
-                // the hit tiles' maxima if the proposal is accepted (a tile = a DPP row)
+                // the hit tiles' maxima if the proposal is accepted (a tile = a DPP row): four items
+                // per thread in flight (rays in HBM: ~140 hit tiles, each load a round trip)
                 const int nt = sh.n_tiles;
-                for (int i = tid - 128; i < nt * kTilePts; i += kChainThreads - 256) {
-                    const int sc = v.tile_rec(i / kTilePts).y;  // start << 5 | count
-                    const int q = (sc >> 5) + (i % kTilePts);
-                    unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
-                    if (i % kTilePts < (sc & 31)) {
-                        const double cd = d.cand_d[q], bd = d.best_d[q];
-                        mk = (unsigned long long)__double_as_longlong(d.cand_flag[q] ? cd : bd);
+                constexpr int MU = 4, MS = kChainThreads - 256;
+                if constexpr (SMALL) {  // (~8 hit tiles: one item per thread)
+                    for (int i = tid - 128; i < nt * kTilePts; i += MS) {
+                        const int sc = v.tile_rec(i / kTilePts).y;  // start << 5 | count
+                        const int q = (sc >> 5) + (i % kTilePts);
+                        unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
+                        if (i % kTilePts < (sc & 31)) {
+                            const double cd = d.cand_d[q], bd = d.best_d[q];
+                            mk = (unsigned long long)__double_as_longlong(d.cand_flag[q] ? cd : bd);
+                        }
+                        mk = row_max_u64(mk);
+                        if ((i % kTilePts) == kTilePts - 1) v.ctm[i / kTilePts] = __longlong_as_double((long long)mk);
                     }
-                    mk = row_max_u64(mk);
-                    if ((i % kTilePts) == kTilePts - 1) v.ctm[i / kTilePts] = __longlong_as_double((long long)mk);
+                } else
+                for (int i0 = tid - 128; i0 < nt * kTilePts; i0 += MU * MS) {
+                    int q[MU];
+                    bool in[MU];
+#pragma unroll
+                    for (int u = 0; u < MU; ++u) {
+                        const int i = min(i0 + u * MS, nt * kTilePts - 1);
+                        const int sc = v.tile_rec(i / kTilePts).y;  // start << 5 | count
+                        in[u] = i0 + u * MS < nt * kTilePts && (i % kTilePts) < (sc & 31);
+                        q[u] = in[u] ? (sc >> 5) + (i % kTilePts) : 0;
+                    }
+                    double cd[MU], bd[MU];
+                    unsigned char cf[MU];
+#pragma unroll
+                    for (int u = 0; u < MU; ++u) {
+                        cd[u] = d.cand_d[q[u]];
+                        bd[u] = d.best_d[q[u]];
+                        cf[u] = d.cand_flag[q[u]];
+                    }
+#pragma unroll
+                    for (int u = 0; u < MU; ++u) {
+                        const int i = i0 + u * MS;
+                        if (i >= nt * kTilePts) break;  // (whole rows: the same in the 16 lanes of a tile)
+                        unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
+                        if (in[u]) mk = (unsigned long long)__double_as_longlong(cf[u] ? cd[u] : bd[u]);
+                        mk = row_max_u64(mk);
+                        if ((i % kTilePts) == kTilePts - 1) v.ctm[i / kTilePts] = __longlong_as_double((long long)mk);
+                    }
                 }
             }
             if (prof_on && lane == 0)
@@ -1674,6 +1753,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         d.cy[sk] = pp.y;
                         d.cz[sk] = pp.z;
                     }
+                    if (!SMALL && !nscript && fwd && sh.k0 < n) {  // the running total follows the committed terms
+                        sh.tsum = sh.b_T;
+                        sh.terr = sh.b_E;
+                    }
                     if (bdec == 2) {  // an estimate inside the bracket of phase F
                         phi_r = sh.phi_n;
                         sh.phi_lo = sh.b_lo;
@@ -1745,6 +1828,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
                     sh.spec_ok = 0;
                     sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
+                    if (!SMALL) sh.dsum = sh.dabs = 0.0;
                     sh.n_super[(it + 1) & 1] = 0;  // the other parity's list is refreshed first
                     sh.pts_seen = sh.ray_pts = 0;
                     sh.k0 = n;
