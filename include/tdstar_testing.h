@@ -49,6 +49,12 @@ int tdt_accept(const td_chain_params *prm, int action, double u_accept, double z
  * in LDS when they fit (the 381-ray configs); 1 keeps them in HBM, the path
  * larger geometries take.  Same results either way. */
 int tdt_chain_set_lds_mode(td_chain *ch, int mode);
+/* Device engine, decisions on bounds (DESIGN.md 4.2 phase F): k > 0 takes every
+ * k-th decision of a launch on the exact chi^2 sums, as a decision falling
+ * inside the brackets would (the committed partial sums made exact again from
+ * where accepted proposals left them, with the proposal's terms in place);
+ * 0 (default) only where the brackets require it.  Same results either way. */
+int tdt_chain_set_exact_every(td_chain *ch, int k);
 /* td_evaluate's resident server (incremental.cpp): sleep `ms` between the
  * host's alive check and the post of every command, so the kernel's 200 ms
  * idle watchdog can fire first (the race of a descheduled host thread).  The

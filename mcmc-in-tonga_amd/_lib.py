@@ -91,6 +91,7 @@ SIGNATURES = {
     "tdt_set_nn_method": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_nn_bench": (ctypes.c_int, [_vp, _pd, _pd, _pd, _pd, _i64, ctypes.c_int, ctypes.c_int, _pd]),
     "tdt_chain_set_lds_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "tdt_chain_set_exact_every": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_exact_sum": (ctypes.c_int, [ctypes.c_int, _pd, _i64, _d, _pd, _pd, _pi32]),
     "tdt_wave_delta_sum": (ctypes.c_int, [ctypes.c_int, _pd, _pd, _pi32, _i64, _d, _pd, _pd]),
     "tdt_block_delta_sum": (ctypes.c_int, [ctypes.c_int, _pd, _pd, _pd, _pi32, _i64, _i64, _pd, _pd,

@@ -1252,6 +1252,13 @@ int tdt_chain_set_lds_mode(td_chain *ch, int mode) {
     return TD_OK;
 }
 
+int tdt_chain_set_exact_every(td_chain *ch, int k) {
+    if (!ch || ch->engine != TD_ENGINE_DEVICE || k < 0) return TD_ERR_ARG;
+    ch->dev.exact_every = k;
+    ch->desc_dirty = true;
+    return TD_OK;
+}
+
 int tdt_chain_lds(td_chain *ch, int64_t out[4]) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE || !out) return TD_ERR_ARG;
     chain_lds_sizes(ch->dev, out);

@@ -106,6 +106,7 @@ struct DevChain {
     uint32_t chain;
     int profile;  // diagnostic phase stamps (s_memtime) -- off in measured runs
     int lds_mode;  // 0: mirror tiles/rays/order in LDS when they fit; 1: always work from HBM (testing)
+    int exact_every;  // testing: > 0 takes every k-th decision on the exact sums, as an undecided bracket would
     // uniform bucket grid over the cells
     CellGrid grid;
     int *bucket_count;      // [G]

@@ -1499,8 +1499,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                             }
                             bdec = __builtin_amdgcn_readfirstlane(bdec);
                             // a tempering round's last iteration publishes phi: decided exactly (and
-                            // every sum made exact) whatever the bounds say
+                            // every sum made exact) whatever the bounds say (testing: every k-th too)
                             if (rbx && it + 1 == round_end) bdec = 0;
+                            if (d.exact_every > 0 && (it % d.exact_every) == d.exact_every - 1) bdec = 0;
                             exact = bdec == 0;
                             phi_n = Sa;  // (an estimate on a decided proposal)
                             if (bdec == 2 && lane == 0) {  // the accepted terms' sums: unformed

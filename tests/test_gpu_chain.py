@@ -333,3 +333,42 @@ def test_library_tempering_loop_equals_round_by_round(tt, ds, ctx):
     for ma, mb, x, y in zip(a[4], b[4], a[5], b[5]):
         assert same_models(ma, mb)
         assert x["phi"] == y["phi"] and x["accepted"] == y["accepted"] and x["proposed"] == y["proposed"]
+
+
+@pytest.mark.parametrize("lds_mode", [0, 1])
+def test_exact_path_of_decisions_on_bounds(tt, ds, ctx, lds_mode):
+    """Phase F decides on bounds and leaves an accepted proposal's chi^2 partial
+    sums unformed; the exact sums (the committed ones made exact again from
+    where accepted proposals left them, with the proposal's own terms in place,
+    then the proposal's) run only when a decision falls inside the brackets --
+    almost never by itself.  Forced on every k-th decision (k = 1, 2, 3, 7,
+    mixing them with bound decisions in every pattern), the chain must be the
+    default chain and the HOST engine's, bit for bit, in both layouts, over
+    several launches (each ends exact); and the state must equal a from-scratch
+    evaluate."""
+    prm = tt.define_TDstructrure().replace(max_cells=1200)
+    model = tt.random_model(1000, 31)
+    L = tt.lib()
+    host = make(tt, ctx, prm, model, 31, tt.TD_ENGINE_HOST)
+    devs = []
+    for k in (0, 1, 2, 3, 7):
+        c = make(tt, ctx, prm, model, 31, tt.TD_ENGINE_DEVICE)
+        assert L.tdt_chain_set_lds_mode(c.h, lds_mode) == 0
+        assert L.tdt_chain_set_exact_every(c.h, k) == 0
+        devs.append(c)
+    for step in (61, 130, 9):
+        host.run(step)
+        sh = host.stats()
+        for c in devs:
+            c.run(step)
+            sd = c.stats()
+            assert sd["phi"] == sh["phi"], (sd, sh)
+            assert sd["accepted"] == sh["accepted"] and sd["proposed"] == sh["proposed"]
+    assert sum(sh["accepted"]) > 20
+    for c in devs:
+        m = c.model()
+        assert same_models(m, host.model())
+        ptS, phi, _, _ = ctx.evaluate(m.cells())
+        assert phi == m.phi and np.array_equal(ptS, m.ptS)
+        c.close()
+    host.close()
