@@ -263,10 +263,10 @@ constexpr size_t kLdsBudget = 160 * 1024;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool small) {
+__host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool small, int waves = kWaves) {
     LdsPlan L{};
     size_t o = align16(sizeof(Shared));
-    L.scratch = o; o += align16(sizeof(double) * kWaves * 96);
+    L.scratch = o; o += align16(sizeof(double) * waves * 96);
     L.draws = o; o += align16(sizeof(tdchain::Draws) * 64);                     // 64 iterations ahead
     if (!small || kSmallWalk) {  // the chi^2 walk's event words (exact_sum.h): static ones, kept; changed rays
         L.smask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
@@ -811,10 +811,12 @@ __device__ __attribute__((noinline)) double exact_sums(const double *term, doubl
 // SCRIPT: host-given proposals (td_evaluate's incremental path: scripted
 // steps, the resident server); a free-running chain's instance has none of
 // that code on its path.
-template <bool SMALL, bool SCRIPT>
-__global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__restrict__ dptr, long long iters,
+template <bool SMALL, bool SCRIPT, int NTH>
+__global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict__ dptr, long long iters,
                                                              ScriptArgs sa) {
     constexpr bool WALK = !SMALL || kSmallWalk;  // chi^2 by the event walk
+    constexpr int kWv = NTH / 64;  // waves: 8 (one chain per CU), or 4 (rays in HBM: two chains per CU)
+    static_assert(NTH == kChainThreads || (!SMALL && NTH == kChainThreads / 2), "512 threads, or 256 in HBM layout");
     if (sa.pin >= 0) {  // one chain, launched as 8 workgroups: only the one on XCD `pin` runs it
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -823,7 +825,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const DevChain &d = dptr[sa.pin >= 0 ? 0 : blockIdx.x];  // fields read from memory as needed
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Shared &sh = *reinterpret_cast<Shared *>(lds);
-    const LdsPlan L = lds_plan(d.ntiles, d.n, d.cap, SMALL);
+    const LdsPlan L = lds_plan(d.ntiles, d.n, d.cap, SMALL, kWv);
     double(*ray_scratch)[96] = reinterpret_cast<double(*)[96]>(lds + L.scratch);
     tdchain::Draws *draws = reinterpret_cast<tdchain::Draws *>(lds + L.draws);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -871,14 +873,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             CopySeg<int, U> c7{ts, d.tile_start, NT + 1}, c8{tr, d.tile_ray, NT}, c9{ro, d.ray_off, n + 1},
                 c10{od, d.order, d.st->ncells};
             const int most = max(max(3 * NT, NT + 1), max(n + 1, c10.n));
-            for (int b0 = tid; b0 < most; b0 += U * kChainThreads) {
+            for (int b0 = tid; b0 < most; b0 += U * NTH) {
                 c0.load(b0); c1.load(b0); c2.load(b0); c3.load(b0); c4.load(b0); c5.load(b0);
                 c6.load(b0); c7.load(b0); c8.load(b0); c9.load(b0); c10.load(b0);
                 c0.store(b0); c1.store(b0); c2.store(b0); c3.store(b0); c4.store(b0); c5.store(b0);
                 c6.store(b0); c7.store(b0); c8.store(b0); c9.store(b0); c10.store(b0);
             }
         }
-        for (int i = tid; i < n; i += kChainThreads) rf[i] = 0;
+        for (int i = tid; i < n; i += NTH) rf[i] = 0;
         v.tlo = a; v.thi = b; v.tmaxd = m; v.tstart = ts; v.ray_off = ro; v.ptS = p; v.prefix = pf; v.tS = t;
         v.sig = sg; v.rflag = rf; v.ord = od;
         v.cptS = reinterpret_cast<double *>(lds + L.cptS);
@@ -896,7 +898,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     // proposal recomputes only the terms of the rays it changes
     {
         double part = 0.0;  // (rays in HBM: their sum in any order, the running total of phase F)
-        for (int r = tid; r < n; r += kChainThreads) {
+        for (int r = tid; r < n; r += NTH) {
             const double df = v.ptS[r] - v.tS[r];
             const double sg = v.sig[r];
             const double t = ((df * df) * 1.0) / (sg * sg);
@@ -944,16 +946,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
     const bool super_on = !SMALL && L.super_lds;
     if constexpr (WALK) {  // the chi^2 walk's static event words of the current state
         if constexpr (SMALL) __syncthreads();  // the terms above
-        delta_marks(v.term, v.prefix, nullptr, n, smask, wv, delta_words(n), kWaves, lane);
-        for (int w = tid; w < delta_words(n); w += kChainThreads) cmask[w] = 0ull;
+        delta_marks(v.term, v.prefix, nullptr, n, smask, wv, delta_words(n), kWv, lane);
+        for (int w = tid; w < delta_words(n); w += NTH) cmask[w] = 0ull;
     }
     if constexpr (!SMALL) {
         if (super_on) {  // super-tile boxes, and maxima = the max of their tiles' maxima
-            for (int i = tid; i < 3 * NS; i += kChainThreads) {
+            for (int i = tid; i < 3 * NS; i += NTH) {
                 slo[i] = d.super_lo[i];
                 shi[i] = d.super_hi[i];
             }
-            for (int S = tid; S < NS; S += kChainThreads) {
+            for (int S = tid; S < NS; S += NTH) {
                 double m = 0.0;
                 for (int t = S * kTilePts; t < min(NT, (S + 1) * kTilePts); ++t) m = fmax(m, d.tile_maxd[t]);
                 smax[S] = f32_up(m);
@@ -1031,7 +1033,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         sh.phi_lo = sh.phi_hi = phi_r;
         if constexpr (!SMALL) {
             double T = 0.0;
-            for (int w = 0; w < kWaves; ++w) T = T + sh.wpart[w];
+            for (int w = 0; w < kWv; ++w) T = T + sh.wpart[w];
             sh.tsum = T;
             sh.terr = kSumSlack * (double)(n + 1) * fabs(T);  // (any order: within (n - 1) ulps of the exact sum)
         }
@@ -1060,7 +1062,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         if constexpr (WALK) {
             // the previous accepted proposal's partial sums (read again only in phase F,
             // after at least one barrier): off its critical path, before this one's tiles
-            if (pend_r) delta_commit<SMALL ? 1 : 16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
+            if (pend_r) delta_commit<SMALL ? 1 : 16>(v.prefix, v.cprefix, n, sh.dseg, tid, NTH);
             pend_r = false;
         }
         if constexpr (!SMALL) {
@@ -1069,7 +1071,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     const unsigned long long mk = row_max_u64(sup_mk);
                     if ((tid & 15) == 15) smax[sup_S] = f32_up(__longlong_as_double((long long)mk));
                 }
-                for (int i = (tid >> 4) + kChainThreads / kTilePts; i < sup_n; i += kChainThreads / kTilePts) {
+                for (int i = (tid >> 4) + NTH / kTilePts; i < sup_n; i += NTH / kTilePts) {
                     const int S = sup_all ? i : shit[sup_par * kListLds + i], t = S * kTilePts + (tid & 15);
                     unsigned long long mk = t < NT ? (unsigned long long)__double_as_longlong(d.tile_maxd[t]) : 0ull;
                     mk = row_max_u64(mk);
@@ -1107,7 +1109,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 const bool q0 = action != tdchain::kBirth;  // old site of the selected cell
                 const bool q1 = action == tdchain::kBirth || action == tdchain::kMove;  // new site
                 const TileQuery tq0 = tile_query(kx, ky, kz), tq1 = tile_query(p.x, p.y, p.z);
-                const int nthr = query ? kChainThreads - 64 : kChainThreads;
+                const int nthr = query ? NTH - 64 : NTH;
                 // tiles in flight per thread: LDS latency is short; HBM needs more
                 constexpr int TU = SMALL ? 3 : 8;
                 if (super_on) {
@@ -1235,11 +1237,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     }
             }
             if (action == tdchain::kDeath) {  // deleteat! shift, staged before we know if it is accepted
-                const int sthr = query ? kChainThreads - 64 : kChainThreads;  // not the query wave: it starts at once
+                const int sthr = query ? NTH - 64 : NTH;  // not the query wave: it starts at once
                 if (tid < sthr)
                     for (int j = (int)p.index + 1 + tid; j < ncells; j += sthr) d.order_tmp[j] = v.ord[j];
             }
-            if (query && wv == kWaves - 1) {  // TD_inversion_function.jl:81 (birth), :146 (death)
+            if (query && wv == kWv - 1) {  // TD_inversion_function.jl:81 (birth), :146 (death)
                 const bool birth = action == tdchain::kBirth;
                 const Nearest r = wave_nearest(d, v, sh, lane, birth ? p.x : kx, birth ? p.y : ky, birth ? p.z : kz,
                                                birth ? -1 : slot_k, -1, 0.0, 0.0, 0.0);
@@ -1289,7 +1291,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         ++seen;
                         point(pre_q, pre_ray, pre_s, pre_bd, pre_x, pre_y, pre_z);
                     }
-                    for (int item = tid; item < nt * kTilePts; item += kChainThreads) {
+                    for (int item = tid; item < nt * kTilePts; item += NTH) {
                         const int t = v.thit[item / kTilePts];
                         if (t < 0) continue;  // preloaded
                         const int sc = v.tstart[t];  // start << 5 | count
@@ -1304,12 +1306,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                     }
                 } else {
                     constexpr int CU = 4;  // items in flight per thread (rays in HBM: latency)
-                    for (int item0 = tid; item0 < nt * kTilePts; item0 += CU * kChainThreads) {
+                    for (int item0 = tid; item0 < nt * kTilePts; item0 += CU * NTH) {
                         int qq[CU], rr[CU], ss[CU];
                         double bb[CU], xx[CU], yy[CU], zz[CU];
 #pragma unroll
                         for (int u = 0; u < CU; ++u) {  // every load of the CU items: one round trip
-                            const int item = item0 + u * kChainThreads;
+                            const int item = item0 + u * NTH;
                             const int4 rec = v.tile_rec(min(item, nt * kTilePts - 1) / kTilePts);
                             const int sc = rec.y;  // start << 5 | count
                             const bool in = item < nt * kTilePts && item % kTilePts < (sc & 31);
@@ -1336,7 +1338,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // ========= phase D: re-search orphaned points, one wave each =========
                 no = sh.n_orphans;
                 const bool death = action == tdchain::kDeath;
-                for (int o = wv; o < no; o += kWaves) {  // one wave per orphan, no block barrier
+                for (int o = wv; o < no; o += kWv) {  // one wave per orphan, no block barrier
                     double qx, qy, qz;
                     int q, ray;
                     if (o < kOrphanLds) {
@@ -1365,15 +1367,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 // in one round of loads before its first sum (the 64 first; more: per ray)
                 int ra = 0, s0a = 0, e0a = 0;
                 double tsa = 0.0, sga = 0.0, ota = 0.0;
-                if (!SMALL && wv + kWaves * lane < nr && lane < 64) {
-                    ra = v.ray_at(wv + kWaves * lane);
+                if (!SMALL && wv + kWv * lane < nr && lane < 64) {
+                    ra = v.ray_at(wv + kWv * lane);
                     s0a = v.ray_off[ra];
                     e0a = v.ray_off[ra + 1];
                     tsa = v.tS[ra];
                     sga = v.sig[ra];
                     ota = v.term[ra];
                 }
-                for (int rr = wv, j = 0; rr < nr; rr += kWaves, ++j) {
+                for (int rr = wv, j = 0; rr < nr; rr += kWv, ++j) {
                     int r, s0, npr;
                     double tsr, sgr, old_term;
                     if (!SMALL && j < 64) {
@@ -1432,13 +1434,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                 if (!nscript && fwd && sh.k0 < n && anchor) {  // (block-uniform)
                     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
                     int k = tid;
-                    for (; k + 3 * kChainThreads < n; k += 4 * kChainThreads) {
+                    for (; k + 3 * NTH < n; k += 4 * NTH) {
                         p0 = p0 + gload(v.term + k);
-                        p1 = p1 + gload(v.term + k + kChainThreads);
-                        p2 = p2 + gload(v.term + k + 2 * kChainThreads);
-                        p3 = p3 + gload(v.term + k + 3 * kChainThreads);
+                        p1 = p1 + gload(v.term + k + NTH);
+                        p2 = p2 + gload(v.term + k + 2 * NTH);
+                        p3 = p3 + gload(v.term + k + 3 * NTH);
                     }
-                    for (; k < n; k += kChainThreads) p0 = p0 + gload(v.term + k);
+                    for (; k < n; k += NTH) p0 = p0 + gload(v.term + k);
                     const double wsum = wave_sum_f64((p0 + p1) + (p2 + p3));
                     if (lane == 0) sh.wpart[wv] = wsum;
                     __syncthreads();
@@ -1476,7 +1478,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                             if (anchor) {
                                 Sa = 0.0;
                                 if constexpr (WALK) {
-                                    for (int w = 0; w < kWaves; ++w) Sa = Sa + sh.wpart[w];
+                                    for (int w = 0; w < kWv; ++w) Sa = Sa + sh.wpart[w];
                                 } else {
                                     double part = 0.0;
                                     for (int k = lane; k < n; k += 64) part = part + v.term[k];
@@ -1559,40 +1561,44 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                                   d.cy, d.cz, d.czeta, [&](int pos) { return v.ord[pos]; });
                     sh.spec_ok = 1;
                 }
-            } else if (wv == kWaves - 1) {  // the grid data an accepted update will need
-                if (action != tdchain::kChange)
+            } else if (wv == kWv - 1 || (kWv >= 6 && wv == kWv - 2)) {
+                // wave kWv - 1: the grid data an accepted update will need; wave kWv - 2 (with 8 waves;
+                // with 4 the last wave after its prefetch): accounting and the model-size factors
+                if (wv == kWv - 1 && action != tdchain::kChange)
                     grid_prefetch(d, sh, lane, action, action == tdchain::kBirth ? new_slot : slot_k, kx, ky,
                                   kz, pp.x, pp.y, pp.z);
-            } else if (wv == kWaves - 2) {
-                if (prof_on && lane == 0) {  // diagnostic: work sizes
-                    sh.prof[68] += sh.n_tiles;
-                    sh.prof[69] += sh.pts_seen;
-                    sh.prof[70] += sh.n_changed;
-                    sh.prof[71] += sh.n_rays;
+                if (wv == (kWv >= 6 ? kWv - 2 : kWv - 1)) {
+                    if (prof_on && lane == 0) {  // diagnostic: work sizes
+                        sh.prof[68] += sh.n_tiles;
+                        sh.prof[69] += sh.pts_seen;
+                        sh.prof[70] += sh.n_changed;
+                        sh.prof[71] += sh.n_rays;
+                    }
+                    if (lane == 0 && fwd) {  // accounting, off wave 0's path
+                        atomicAdd((unsigned long long *)&sh.evaluations, 1ull);
+                        // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
+                        // candidate points (coords + cached slot/distance, 36 B), grid queries
+                        // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
+                        // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
+                        atomicAdd((unsigned long long *)&sh.bytes,
+                                  (unsigned long long)((super_on ? (long long)NS * 32 +
+                                                                      (long long)sh.n_super[it & 1] * kTilePts * 32
+                                                                 : (long long)NT * 32) +
+                                                       (long long)sh.pts_seen * 36 +
+                                                       (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
+                                                       (long long)sh.ray_pts * 17 + (long long)(n - sh.k0) * 28));
+                    }
+                    if (lane == 0 && (action == tdchain::kBirth || action == tdchain::kDeath)) {
+                        sh.lnN_far[0] = d.logN[max(ncells - 2, 0)];
+                        sh.lnN_far[1] = d.logN[ncells + 2];
+                    }
                 }
-                if (lane == 0 && fwd) {  // accounting, off wave 0's path
-                    atomicAdd((unsigned long long *)&sh.evaluations, 1ull);
-                    // bytes this proposal's algorithm must read: tile boxes + maxima (32 B),
-                    // candidate points (coords + cached slot/distance, 36 B), grid queries
-                    // (27 buckets x 8 entries x 32 B), rays (w, zeta, flag: 17 B per point),
-                    // chi^2 tail (ptS, tS, sig, flag: 28 B per ray)
-                    atomicAdd((unsigned long long *)&sh.bytes,
-                              (unsigned long long)((super_on ? (long long)NS * 32 +
-                                                                  (long long)sh.n_super[it & 1] * kTilePts * 32
-                                                             : (long long)NT * 32) +
-                                                   (long long)sh.pts_seen * 36 +
-                                                   (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
-                                                   (long long)sh.ray_pts * 17 + (long long)(n - sh.k0) * 28));
-                }
-                if (lane == 0 && (action == tdchain::kBirth || action == tdchain::kDeath)) {
-                    sh.lnN_far[0] = d.logN[max(ncells - 2, 0)];
-                    sh.lnN_far[1] = d.logN[ncells + 2];
-                }
-            } else if (wv >= 2 && wv <= kWaves - 3 && fwd && action != tdchain::kChange) {  // waves 2..5
-                // the hit tiles' maxima if the proposal is accepted (a tile = a DPP row): four items
-                // per thread in flight (rays in HBM: ~140 hit tiles, each load a round trip)
+            } else if (wv >= 2 && wv <= (kWv >= 6 ? kWv - 3 : 2) && fwd && action != tdchain::kChange) {
+                // (waves 2..5 of 8, wave 2 of 4) the hit tiles' maxima if the proposal is accepted (a tile =
+                // a DPP row): four items per thread in flight (rays in HBM: ~140 hit tiles, each load a
+                // round trip)
                 const int nt = sh.n_tiles;
-                constexpr int MU = 4, MS = kChainThreads - 256;
+                constexpr int MU = 4, MS = (kWv >= 6 ? kWv - 4 : 1) * 64;
                 if constexpr (SMALL) {  // (~8 hit tiles: one item per thread)
                     for (int i = tid - 128; i < nt * kTilePts; i += MS) {
                         const int sc = v.tile_rec(i / kTilePts).y;  // start << 5 | count
@@ -1674,7 +1680,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             // the changed points' global records (two dependent L2 round trips) and the
             // deleteat! shift go to waves 1.., so wave 0 goes straight to its scalars and
             // the next proposal (kW threads, index w = tid - 64)
-            constexpr int kW = kChainThreads - 64;
+            constexpr int kW = NTH - 64;
             const int w = tid - 64;
             if (sh.accept) {
                 const int nt = sh.n_tiles, k0 = sh.k0;
@@ -1687,17 +1693,17 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         d.cand_flag[q] = 0;
                     }
                 if (fwd && action != tdchain::kChange) {
-                    for (int i = tid; i < nt; i += kChainThreads) v.tmaxd[v.tile_rec(i).x] = v.ctm[i];
+                    for (int i = tid; i < nt; i += NTH) v.tmaxd[v.tile_rec(i).x] = v.ctm[i];
                     pend_sup = super_on;  // their super-tiles' maxima: at the top of the next iteration
                 }
-                for (int rr = tid; rr < nr; rr += kChainThreads) {
+                for (int rr = tid; rr < nr; rr += NTH) {
                     const int r = v.ray_at(rr);
                     v.ptS[r] = v.cptS[r];
                     v.rflag[r] = 0;
                 }
                 if (!WALK || !nscript) {
                     if (!sh.defer)  // (accepted on bounds: its partial sums are left unformed)
-                        for (int r = k0 + tid; r < n; r += kChainThreads) v.prefix[r] = v.cprefix[r];
+                        for (int r = k0 + tid; r < n; r += NTH) v.prefix[r] = v.cprefix[r];
                 } else if (fwd && k0 < n) {
                     pend_r = true;  // written at the top of the next iteration
                     if (wv == 1) delta_remark(v.term, v.prefix, v.cprefix, n, sh.dseg, smask, lane);
@@ -1718,7 +1724,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
                         }
                     }
                 }
-                if (tid == kChainThreads - 64 && sh.g_op) grid_apply(d, sh);
+                if (tid == NTH - 64 && sh.g_op) grid_apply(d, sh);
                 if (tid == 0) {
                     const int sk = slot_k;
                     if (action == tdchain::kBirth) {  // append!
@@ -1771,7 +1777,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
             } else {  // rejected: flags down, the changed rays get their old chi^2 terms back
                 if (wv != 0)
                     for (int c = w; c < nc; c += kW) d.cand_flag[d.changed[c]] = 0;
-                for (int rr = tid; rr < nr; rr += kChainThreads) {
+                for (int rr = tid; rr < nr; rr += NTH) {
                     const int r = v.ray_at(rr);
                     v.term[r] = v.cterm[r];
                     v.rflag[r] = 0;
@@ -1853,17 +1859,17 @@ __global__ __launch_bounds__(kChainThreads) void k_chain_run(const DevChain *__r
         __syncthreads();
     }
     if constexpr (WALK) {
-        if (pend_r) delta_commit<SMALL ? 1 : 16>(v.prefix, v.cprefix, n, sh.dseg, tid, kChainThreads);
+        if (pend_r) delta_commit<SMALL ? 1 : 16>(v.prefix, v.cprefix, n, sh.dseg, tid, NTH);
         if constexpr (SMALL) __syncthreads();  // the LDS sums are written back below
     }
     // ---- leave the LDS copies behind (flags and grid are already clean) ----
     if constexpr (SMALL) {
-        for (int i = tid; i < NT; i += kChainThreads) d.tile_maxd[i] = v.tmaxd[i];
-        for (int i = tid; i < n; i += kChainThreads) {
+        for (int i = tid; i < NT; i += NTH) d.tile_maxd[i] = v.tmaxd[i];
+        for (int i = tid; i < n; i += NTH) {
             d.ptS[i] = v.ptS[i];
             d.prefix[i] = v.prefix[i];
         }
-        for (int i = tid; i < sh.ncells; i += kChainThreads) d.order[i] = v.ord[i];
+        for (int i = tid; i < sh.ncells; i += NTH) d.order[i] = v.ord[i];
     }
     if (tid == 0) {
         ChainScalars &s = *d.st;
@@ -2076,19 +2082,24 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
     }
     // one LDS size for the whole grid: the largest plan of any chain; the
     // small (LDS-mirrored) variant only if every chain fits
-    size_t small = 0, big = 0;
-    bool force_hbm = false;
+    size_t small = 0, big = 0, half = 0;
+    bool force_hbm = false, packed = true;  // packed: every chain asks for two chains per CU (lds_mode 2)
     for (int b = 0; b < nchains; ++b) {
         const DevChain &d = host[b];
         small = std::max(small, lds_plan(d.ntiles, d.n, d.cap, true).total);
         big = std::max(big, lds_plan(d.ntiles, d.n, d.cap, false).total);
-        force_hbm = force_hbm || d.lds_mode == 1;
+        half = std::max(half, lds_plan(d.ntiles, d.n, d.cap, false, kWaves / 2).total);
+        force_hbm = force_hbm || d.lds_mode >= 1;
+        packed = packed && d.lds_mode == 2;
     }
     const bool scripted = sa.n > 0 || sa.mb != nullptr;
     static bool attr_set = false;  // dynamic LDS above 64 KB needs the attribute (once per kernel)
     if (!attr_set) {
-        for (const void *k : {(const void *)k_chain_run<true, false>, (const void *)k_chain_run<true, true>,
-                              (const void *)k_chain_run<false, false>, (const void *)k_chain_run<false, true>}) {
+        for (const void *k : {(const void *)k_chain_run<true, false, kChainThreads>,
+                              (const void *)k_chain_run<true, true, kChainThreads>,
+                              (const void *)k_chain_run<false, false, kChainThreads>,
+                              (const void *)k_chain_run<false, true, kChainThreads>,
+                              (const void *)k_chain_run<false, false, kChainThreads / 2>}) {
             hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
             if (e != hipSuccess) return e;
         }
@@ -2096,18 +2107,22 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
     }
     if (small <= kLdsBudget && !force_hbm) {
         if (scripted)
-            hipLaunchKernelGGL((k_chain_run<true, true>), dim3(grid), dim3(kChainThreads), small, s, dev,
-                               (long long)iters, sa);
+            hipLaunchKernelGGL((k_chain_run<true, true, kChainThreads>), dim3(grid), dim3(kChainThreads), small, s,
+                               dev, (long long)iters, sa);
         else
-            hipLaunchKernelGGL((k_chain_run<true, false>), dim3(grid), dim3(kChainThreads), small, s, dev,
-                               (long long)iters, sa);
+            hipLaunchKernelGGL((k_chain_run<true, false, kChainThreads>), dim3(grid), dim3(kChainThreads), small, s,
+                               dev, (long long)iters, sa);
+    } else if (packed && !scripted && half <= kLdsBudget / 2) {
+        // rays in HBM, 4 waves and <= 80 KB of LDS per chain: two chains resident per CU
+        hipLaunchKernelGGL((k_chain_run<false, false, kChainThreads / 2>), dim3(grid), dim3(kChainThreads / 2), half,
+                           s, dev, (long long)iters, sa);
     } else {
         if (scripted)
-            hipLaunchKernelGGL((k_chain_run<false, true>), dim3(grid), dim3(kChainThreads), big, s, dev,
-                               (long long)iters, sa);
+            hipLaunchKernelGGL((k_chain_run<false, true, kChainThreads>), dim3(grid), dim3(kChainThreads), big, s,
+                               dev, (long long)iters, sa);
         else
-            hipLaunchKernelGGL((k_chain_run<false, false>), dim3(grid), dim3(kChainThreads), big, s, dev,
-                               (long long)iters, sa);
+            hipLaunchKernelGGL((k_chain_run<false, false, kChainThreads>), dim3(grid), dim3(kChainThreads), big, s,
+                               dev, (long long)iters, sa);
     }
     return hipGetLastError();
 }
