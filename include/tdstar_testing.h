@@ -47,7 +47,10 @@ int tdt_accept(const td_chain_params *prm, int action, double u_accept, double z
                double phi_n, double czeta, double zeta_killed, double zetanew_death);
 /* Device engine layout: 0 (default) mirrors tiles, rays and the Julia order
  * in LDS when they fit (the 381-ray configs); 1 keeps them in HBM, the path
- * larger geometries take.  Same results either way. */
+ * larger geometries take; 2 runs the 4-wave kernel that puts two chains on a
+ * CU (td_chain_run_batch of more chains than CUs): the tiles in LDS when they
+ * fit in 80 KB, else everything in HBM; 3 (testing) that kernel with
+ * everything in HBM.  Same results either way. */
 int tdt_chain_set_lds_mode(td_chain *ch, int mode);
 /* Device engine, decisions on bounds (DESIGN.md 4.2 phase F): k > 0 takes every
  * k-th decision of a launch on the exact chi^2 sums, as a decision falling

@@ -1246,7 +1246,7 @@ int tdt_set_server_post_delay(int ms) {
     return TD_OK;
 }
 int tdt_chain_set_lds_mode(td_chain *ch, int mode) {
-    if (!ch || ch->engine != TD_ENGINE_DEVICE || mode < 0 || mode > 2) return TD_ERR_ARG;
+    if (!ch || ch->engine != TD_ENGINE_DEVICE || mode < 0 || mode > 3) return TD_ERR_ARG;
     ch->dev.lds_mode = mode;
     ch->desc_dirty = true;
     return TD_OK;

@@ -47,7 +47,7 @@ using tdchain::Proposal;
 
 constexpr int kWaves = kChainThreads / 64;
 static_assert(kTilePts == 16, "a tile is one 16-lane DPP row (row_max_u64)");
-constexpr int kOrphanLds = 256; // orphan records kept in LDS (more: read back from HBM)
+constexpr int kOrphanLds = 96;  // orphan records kept in LDS (more: read back from HBM)
 constexpr int kPre = 64 / kTilePts;  // LDS layout: hit tiles per wave whose points phase B preloads
 static_assert(kPre == 4, "the preload slots are four registers");
 constexpr int kListLds = 1024;  // rays in HBM: hit tiles / changed rays / hit super-tiles kept in LDS
@@ -263,7 +263,10 @@ constexpr size_t kLdsBudget = 160 * 1024;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool small, int waves = kWaves) {
+// small: the tiles in LDS (and, rays_lds, the per-ray arrays and the order too -- else those and the
+// hit tiles' candidate maxima stay in HBM: the 4-wave two-chains-per-CU kernel's "tiles" layout)
+__host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool small, int waves = kWaves,
+                                            bool rays_lds = true) {
     LdsPlan L{};
     size_t o = align16(sizeof(Shared));
     L.scratch = o; o += align16(sizeof(double) * waves * 96);
@@ -278,20 +281,22 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
         L.tmaxd = o; o += align16(sizeof(double) * ntiles);
         L.tstart = o; o += align16(sizeof(int) * (ntiles + 1));
         L.thit = o; o += align16(sizeof(int) * (ntiles + 1));
-        L.ctm = o; o += align16(sizeof(double) * (ntiles + 1));
+        if (rays_lds) { L.ctm = o; o += align16(sizeof(double) * (ntiles + 1)); }
         L.tray = o; o += align16(sizeof(int) * ntiles);
-        L.rayoff = o; o += align16(sizeof(int) * (n + 1));
-        L.ptS = o; o += align16(sizeof(double) * n);
-        L.prefix = o; o += align16(sizeof(double) * n);
-        L.cptS = o; o += align16(sizeof(double) * n);
-        L.cprefix = o; o += align16(sizeof(double) * n);
-        L.term = o; o += align16(sizeof(double) * n);
-        L.cterm = o; o += align16(sizeof(double) * n);
-        L.tS = o; o += align16(sizeof(double) * n);
-        L.sig = o; o += align16(sizeof(double) * n);
-        L.rflag = o; o += align16(sizeof(int) * n);
-        L.rhit = o; o += align16(sizeof(int) * n);
-        L.ord = o; o += align16(sizeof(int) * cap);
+        if (rays_lds) {
+            L.rayoff = o; o += align16(sizeof(int) * (n + 1));
+            L.ptS = o; o += align16(sizeof(double) * n);
+            L.prefix = o; o += align16(sizeof(double) * n);
+            L.cptS = o; o += align16(sizeof(double) * n);
+            L.cprefix = o; o += align16(sizeof(double) * n);
+            L.term = o; o += align16(sizeof(double) * n);
+            L.cterm = o; o += align16(sizeof(double) * n);
+            L.tS = o; o += align16(sizeof(double) * n);
+            L.sig = o; o += align16(sizeof(double) * n);
+            L.rflag = o; o += align16(sizeof(int) * n);
+            L.rhit = o; o += align16(sizeof(int) * n);
+            L.ord = o; o += align16(sizeof(int) * cap);
+        }
     } else {
         // the first hit tiles as {tile, start << 5 | count, ray} records, the first changed rays
         size_t q = o;
@@ -595,22 +600,6 @@ __device__ __forceinline__ float f32_up(double x) {
     return (double)f < x ? __int_as_float(__float_as_int(f) + 1) : f;  // f >= 0 finite: the next float up
 }
 
-// dst[0..count) = src[0..count), the whole block: U loads in flight per thread
-// before any store (one memory round trip per U * kChainThreads elements --
-// the launch preamble is latency-bound, not bandwidth-bound)
-template <class T>
-__device__ __forceinline__ void block_copy(T *dst, const T *__restrict__ src, int count, int tid) {
-    constexpr int U = 8;
-    for (int b = tid; b < count; b += U * kChainThreads) {
-        T v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = src[min(b + u * kChainThreads, count - 1)];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (b + u * kChainThreads < count) dst[b + u * kChainThreads] = v[u];
-    }
-}
-
 // System-scope access to the mailbox (pinned host memory, the host polls it)
 __device__ __forceinline__ long long mb_load(const long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -749,8 +738,9 @@ __device__ void round_wait(RoundBox *rb, int b, Shared &sh, int lane, bool publi
 // One array of a fused block copy: U elements per thread per round, loaded
 // into registers by load(), written by store().  Several Segs loaded before
 // any is stored keep all their loads in flight at once: the launch preamble
-// is a handful of memory round trips whatever the number of arrays.
-template <class T, int U>
+// is a handful of memory round trips whatever the number of arrays.  S = the
+// block's thread count (the caller's loop steps by U * S).
+template <class T, int U, int S = kChainThreads>
 struct CopySeg {
     T *dst;
     const T *src;
@@ -759,12 +749,12 @@ struct CopySeg {
     __device__ __forceinline__ void load(int b) {
         if (n <= 0) return;
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = src[min(b + u * kChainThreads, n - 1)];
+        for (int u = 0; u < U; ++u) v[u] = src[min(b + u * S, n - 1)];
     }
     __device__ __forceinline__ void store(int b) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (b + u * kChainThreads < n) dst[b + u * kChainThreads] = v[u];
+            if (b + u * S < n) dst[b + u * S] = v[u];
     }
 };
 
@@ -811,12 +801,16 @@ __device__ __attribute__((noinline)) double exact_sums(const double *term, doubl
 // SCRIPT: host-given proposals (td_evaluate's incremental path: scripted
 // steps, the resident server); a free-running chain's instance has none of
 // that code on its path.
-template <bool SMALL, bool SCRIPT, int NTH>
+// SMALL: the tiles mirrored in LDS (else in HBM, with super-tiles); RLDS: the per-ray arrays and the
+// Julia order mirrored too (the 381-ray configs, 8 waves); NTH: 512 threads, or 256 (two chains per CU)
+template <bool SMALL, bool SCRIPT, int NTH, bool RLDS = SMALL>
 __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict__ dptr, long long iters,
                                                              ScriptArgs sa) {
     constexpr bool WALK = !SMALL || kSmallWalk;  // chi^2 by the event walk
     constexpr int kWv = NTH / 64;  // waves: 8 (one chain per CU), or 4 (rays in HBM: two chains per CU)
-    static_assert(NTH == kChainThreads || (!SMALL && NTH == kChainThreads / 2), "512 threads, or 256 in HBM layout");
+    static_assert(!RLDS || SMALL, "rays in LDS only with the tiles in LDS");
+    static_assert(NTH == kChainThreads || (!RLDS && !SCRIPT && NTH == kChainThreads / 2),
+                  "512 threads, or 256 with the rays in HBM");
     if (sa.pin >= 0) {  // one chain, launched as 8 workgroups: only the one on XCD `pin` runs it
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -825,7 +819,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     const DevChain &d = dptr[sa.pin >= 0 ? 0 : blockIdx.x];  // fields read from memory as needed
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Shared &sh = *reinterpret_cast<Shared *>(lds);
-    const LdsPlan L = lds_plan(d.ntiles, d.n, d.cap, SMALL, kWv);
+    const LdsPlan L = lds_plan(d.ntiles, d.n, d.cap, SMALL, kWv, RLDS);
     double(*ray_scratch)[96] = reinterpret_cast<double(*)[96]>(lds + L.scratch);
     tdchain::Draws *draws = reinterpret_cast<tdchain::Draws *>(lds + L.draws);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -856,7 +850,25 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     v.term = d.term;
     v.cterm = d.cand_term;
     v.ctm = d.tile_cmax;
-    if constexpr (SMALL) {
+    if constexpr (SMALL && !RLDS) {  // the tiles only (the rays, the order, the candidate maxima in HBM)
+        float *a = reinterpret_cast<float *>(lds + L.tlo), *b = reinterpret_cast<float *>(lds + L.thi);
+        double *m = reinterpret_cast<double *>(lds + L.tmaxd);
+        int *ts = reinterpret_cast<int *>(lds + L.tstart), *tr = reinterpret_cast<int *>(lds + L.tray);
+        {
+            constexpr int U = 4;
+            CopySeg<float, U, NTH> c0{a, d.tile_lo, 3 * NT}, c1{b, d.tile_hi, 3 * NT};
+            CopySeg<double, U, NTH> c2{m, d.tile_maxd, NT};
+            CopySeg<int, U, NTH> c7{ts, d.tile_start, NT + 1}, c8{tr, d.tile_ray, NT};
+            for (int b0 = tid; b0 < 3 * NT; b0 += U * NTH) {
+                c0.load(b0); c1.load(b0); c2.load(b0); c7.load(b0); c8.load(b0);
+                c0.store(b0); c1.store(b0); c2.store(b0); c7.store(b0); c8.store(b0);
+            }
+        }
+        v.tlo = a; v.thi = b; v.tmaxd = m; v.tstart = ts; v.tray = tr;
+        v.thit = reinterpret_cast<int *>(lds + L.thit);
+        __syncthreads();
+    }
+    if constexpr (RLDS) {
         float *a = reinterpret_cast<float *>(lds + L.tlo), *b = reinterpret_cast<float *>(lds + L.thi);
         double *m = reinterpret_cast<double *>(lds + L.tmaxd);
         int *ts = reinterpret_cast<int *>(lds + L.tstart), *ro = reinterpret_cast<int *>(lds + L.rayoff);
@@ -867,10 +879,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         v.tray = tr;
         {  // every mirror in one fused copy (positions >= ncells of the order are written before read)
             constexpr int U = 4;
-            CopySeg<float, U> c0{a, d.tile_lo, 3 * NT}, c1{b, d.tile_hi, 3 * NT};
-            CopySeg<double, U> c2{m, d.tile_maxd, NT}, c3{p, d.ptS, n}, c4{pf, d.prefix, n}, c5{t, d.tS, n},
+            CopySeg<float, U, NTH> c0{a, d.tile_lo, 3 * NT}, c1{b, d.tile_hi, 3 * NT};
+            CopySeg<double, U, NTH> c2{m, d.tile_maxd, NT}, c3{p, d.ptS, n}, c4{pf, d.prefix, n}, c5{t, d.tS, n},
                 c6{sg, d.sig, n};
-            CopySeg<int, U> c7{ts, d.tile_start, NT + 1}, c8{tr, d.tile_ray, NT}, c9{ro, d.ray_off, n + 1},
+            CopySeg<int, U, NTH> c7{ts, d.tile_start, NT + 1}, c8{tr, d.tile_ray, NT}, c9{ro, d.ray_off, n + 1},
                 c10{od, d.order, d.st->ncells};
             const int most = max(max(3 * NT, NT + 1), max(n + 1, c10.n));
             for (int b0 = tid; b0 < most; b0 += U * NTH) {
@@ -905,7 +917,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             v.term[r] = t;
             part = part + t;
         }
-        if constexpr (!SMALL) {
+        if constexpr (!RLDS) {
             part = wave_sum_f64(part);
             if (lane == 0) sh.wpart[wv] = part;
         }
@@ -917,7 +929,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         sh.bytes = 0;
         sh.cur = 0;
         sh.defer = 0;
-        if (!SMALL) sh.dsum = sh.dabs = 0.0;
+        if (!RLDS) sh.dsum = sh.dabs = 0.0;
         sh.grid_fallbacks32 = 0;
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
@@ -1031,7 +1043,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     if (tid == 0) {
         sh.ex_upto = n;
         sh.phi_lo = sh.phi_hi = phi_r;
-        if constexpr (!SMALL) {
+        if constexpr (!RLDS) {
             double T = 0.0;
             for (int w = 0; w < kWv; ++w) T = T + sh.wpart[w];
             sh.tsum = T;
@@ -1367,7 +1379,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 // in one round of loads before its first sum (the 64 first; more: per ray)
                 int ra = 0, s0a = 0, e0a = 0;
                 double tsa = 0.0, sga = 0.0, ota = 0.0;
-                if (!SMALL && wv + kWv * lane < nr && lane < 64) {
+                if (!RLDS && wv + kWv * lane < nr && lane < 64) {
                     ra = v.ray_at(wv + kWv * lane);
                     s0a = v.ray_off[ra];
                     e0a = v.ray_off[ra + 1];
@@ -1378,7 +1390,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 for (int rr = wv, j = 0; rr < nr; rr += kWv, ++j) {
                     int r, s0, npr;
                     double tsr, sgr, old_term;
-                    if (!SMALL && j < 64) {
+                    if (!RLDS && j < 64) {
                         r = __builtin_amdgcn_readlane(ra, j);
                         s0 = __builtin_amdgcn_readlane(s0a, j);
                         npr = __builtin_amdgcn_readlane(e0a, j) - s0;
@@ -1401,7 +1413,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         v.cterm[r] = old_term;                       // kept to undo a rejection
                         const double nterm = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                         v.term[r] = nterm;
-                        if constexpr (!SMALL) {  // (the running total: any order; rays in LDS re-add them all)
+                        if constexpr (!RLDS) {  // (the running total: any order; rays in LDS re-add them all)
                             atomicAdd(&sh.dsum, nterm - old_term);
                             atomicAdd(&sh.dabs, fabs(nterm) + fabs(old_term));
                         }
@@ -1425,9 +1437,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             // sum is formed afresh from all the terms (block-uniform: every lane reads the same LDS).
             // Rays in LDS: the ~400 terms are re-added every time (one wave, one DPP reduction: as
             // cheap as keeping the total).
-            const double Tp = SMALL ? 0.0 : sh.tsum + sh.dsum;
-            const double Ep = SMALL ? 0.0 : sh.terr + kSumSlack * ((double)(sh.n_rays + 2) * sh.dabs + fabs(Tp));
-            const bool anchor = SMALL || !(Ep <= 1e-10 * Tp);
+            const double Tp = RLDS ? 0.0 : sh.tsum + sh.dsum;
+            const double Ep = RLDS ? 0.0 : sh.terr + kSumSlack * ((double)(sh.n_rays + 2) * sh.dabs + fabs(Tp));
+            const bool anchor = RLDS || !(Ep <= 1e-10 * Tp);
             if constexpr (WALK) {
                 // rays in HBM: the whole block adds the proposal's terms afresh in any order --
                 // n / 512 global loads per thread, four in flight
@@ -1486,7 +1498,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                 }
                                 Ea = kSumSlack * (double)(n + 1) * fabs(Sa);
                             }
-                            if (!SMALL && lane == 0) {  // the running total if the proposal is committed
+                            if (!RLDS && lane == 0) {  // the running total if the proposal is committed
                                 sh.b_T = Sa;
                                 sh.b_E = Ea;
                             }
@@ -1760,7 +1772,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         d.cy[sk] = pp.y;
                         d.cz[sk] = pp.z;
                     }
-                    if (!SMALL && !nscript && fwd && sh.k0 < n) {  // the running total follows the committed terms
+                    if (!RLDS && !nscript && fwd && sh.k0 < n) {  // the running total follows the committed terms
                         sh.tsum = sh.b_T;
                         sh.terr = sh.b_E;
                     }
@@ -1835,7 +1847,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
                     sh.spec_ok = 0;
                     sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
-                    if (!SMALL) sh.dsum = sh.dabs = 0.0;
+                    if (!RLDS) sh.dsum = sh.dabs = 0.0;
                     sh.n_super[(it + 1) & 1] = 0;  // the other parity's list is refreshed first
                     sh.pts_seen = sh.ray_pts = 0;
                     sh.k0 = n;
@@ -1865,11 +1877,13 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     // ---- leave the LDS copies behind (flags and grid are already clean) ----
     if constexpr (SMALL) {
         for (int i = tid; i < NT; i += NTH) d.tile_maxd[i] = v.tmaxd[i];
-        for (int i = tid; i < n; i += NTH) {
-            d.ptS[i] = v.ptS[i];
-            d.prefix[i] = v.prefix[i];
+        if constexpr (RLDS) {
+            for (int i = tid; i < n; i += NTH) {
+                d.ptS[i] = v.ptS[i];
+                d.prefix[i] = v.prefix[i];
+            }
+            for (int i = tid; i < sh.ncells; i += NTH) d.order[i] = v.ord[i];
         }
-        for (int i = tid; i < sh.ncells; i += NTH) d.order[i] = v.ord[i];
     }
     if (tid == 0) {
         ChainScalars &s = *d.st;
@@ -2082,15 +2096,19 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
     }
     // one LDS size for the whole grid: the largest plan of any chain; the
     // small (LDS-mirrored) variant only if every chain fits
-    size_t small = 0, big = 0, half = 0;
-    bool force_hbm = false, packed = true;  // packed: every chain asks for two chains per CU (lds_mode 2)
+    size_t small = 0, big = 0, half = 0, hyb = 0;
+    // packed: every chain asks for two chains per CU (lds_mode 2: the tiles in LDS when they fit; 3, testing:
+    // the rays-in-HBM 4-wave kernel)
+    bool force_hbm = false, packed = true, tiles_ok = true;
     for (int b = 0; b < nchains; ++b) {
         const DevChain &d = host[b];
         small = std::max(small, lds_plan(d.ntiles, d.n, d.cap, true).total);
         big = std::max(big, lds_plan(d.ntiles, d.n, d.cap, false).total);
         half = std::max(half, lds_plan(d.ntiles, d.n, d.cap, false, kWaves / 2).total);
+        hyb = std::max(hyb, lds_plan(d.ntiles, d.n, d.cap, true, kWaves / 2, false).total);
         force_hbm = force_hbm || d.lds_mode >= 1;
-        packed = packed && d.lds_mode == 2;
+        packed = packed && d.lds_mode >= 2;
+        tiles_ok = tiles_ok && d.lds_mode == 2;
     }
     const bool scripted = sa.n > 0 || sa.mb != nullptr;
     static bool attr_set = false;  // dynamic LDS above 64 KB needs the attribute (once per kernel)
@@ -2099,7 +2117,8 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
                               (const void *)k_chain_run<true, true, kChainThreads>,
                               (const void *)k_chain_run<false, false, kChainThreads>,
                               (const void *)k_chain_run<false, true, kChainThreads>,
-                              (const void *)k_chain_run<false, false, kChainThreads / 2>}) {
+                              (const void *)k_chain_run<false, false, kChainThreads / 2>,
+                              (const void *)k_chain_run<true, false, kChainThreads / 2, false>}) {
             hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
             if (e != hipSuccess) return e;
         }
@@ -2112,6 +2131,11 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
         else
             hipLaunchKernelGGL((k_chain_run<true, false, kChainThreads>), dim3(grid), dim3(kChainThreads), small, s,
                                dev, (long long)iters, sa);
+    } else if (packed && !scripted && tiles_ok && hyb <= kLdsBudget / 2) {
+        // two chains resident per CU (4 waves, <= 80 KB of LDS each): the tiles in LDS, the rays and the
+        // order in HBM
+        hipLaunchKernelGGL((k_chain_run<true, false, kChainThreads / 2, false>), dim3(grid), dim3(kChainThreads / 2),
+                           hyb, s, dev, (long long)iters, sa);
     } else if (packed && !scripted && half <= kLdsBudget / 2) {
         // rays in HBM, 4 waves and <= 80 KB of LDS per chain: two chains resident per CU
         hipLaunchKernelGGL((k_chain_run<false, false, kChainThreads / 2>), dim3(grid), dim3(kChainThreads / 2), half,

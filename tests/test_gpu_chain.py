@@ -374,11 +374,13 @@ def test_exact_path_of_decisions_on_bounds(tt, ds, ctx, lds_mode):
     host.close()
 
 
-def test_two_chains_per_cu_variant_follows_host(tt, ds, ctx):
-    """lds_mode 2: the 256-thread (4-wave) rays-in-HBM kernel whose <= 80 KB of
-    LDS and <= 256 registers let two chains share a CU (td_chain_run_batch
-    packs 2 per CU) -- its wave roles differ from the 8-wave kernel's (phase F:
-    the tile maxima on one wave, the grid prefetch and the accounting on the
+@pytest.mark.parametrize("mode", [2, 3])
+def test_two_chains_per_cu_variant_follows_host(tt, ds, ctx, mode):
+    """lds_mode 2 / 3: the 256-thread (4-wave) kernel whose <= 80 KB of LDS and
+    <= 256 registers let two chains share a CU (td_chain_run_batch packs 2 per
+    CU), with the tiles in LDS and the rays and order in HBM (2), or all in
+    HBM (3) -- its wave roles differ from the 8-wave kernel's (phase F: the
+    tile maxima on one wave, the grid prefetch and the accounting on the
     last).  Alone and batched (more chains than CUs), every chain equals the
     HOST engine and the 8-wave kernel, bit for bit; the state equals a
     from-scratch evaluate."""
@@ -389,7 +391,7 @@ def test_two_chains_per_cu_variant_follows_host(tt, ds, ctx):
     eight = [make(tt, ctx, prm, tt.random_model(n, s), s, tt.TD_ENGINE_DEVICE, chain=s) for n, s in specs]
     four = [make(tt, ctx, prm, tt.random_model(n, s), s, tt.TD_ENGINE_DEVICE, chain=s) for n, s in specs]
     for c in four:
-        assert L.tdt_chain_set_lds_mode(c.h, 2) == 0
+        assert L.tdt_chain_set_lds_mode(c.h, mode) == 0
     for step in (70, 130):
         for c in host + eight:
             c.run(step)
@@ -399,7 +401,7 @@ def test_two_chains_per_cu_variant_follows_host(tt, ds, ctx):
             assert sf["phi"] == se["phi"] == sh["phi"], (sh, se, sf)
             assert sf["accepted"] == sh["accepted"] and sf["proposed"] == sh["proposed"]
     solo = make(tt, ctx, prm, tt.random_model(1000, 71), 71, tt.TD_ENGINE_DEVICE, chain=71)
-    assert L.tdt_chain_set_lds_mode(solo.h, 2) == 0
+    assert L.tdt_chain_set_lds_mode(solo.h, mode) == 0
     solo.run(200)
     assert solo.stats()["phi"] == host[0].stats()["phi"]
     for h, f in zip(host, four):
@@ -411,7 +413,7 @@ def test_two_chains_per_cu_variant_follows_host(tt, ds, ctx):
     many = [make(tt, ctx, prm, tt.random_model(300, 900 + j), 900 + j, tt.TD_ENGINE_DEVICE, chain=900 + j)
             for j in range(300)]
     for c in many:
-        assert L.tdt_chain_set_lds_mode(c.h, 2) == 0
+        assert L.tdt_chain_set_lds_mode(c.h, mode) == 0
     tt.run_batch(many, 60)
     for j in (0, 137, 299):
         ref = make(tt, ctx, prm, tt.random_model(300, 900 + j), 900 + j, tt.TD_ENGINE_HOST, chain=900 + j)

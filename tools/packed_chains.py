@@ -21,8 +21,8 @@ def main():
     prm = tt.define_TDstructrure().replace(max_cells=10000)
     model = tt.random_model(5000, 3)
     out = {}
-    for name, C, mode in (("lds_1perCU", 256, 0), ("hbm_1perCU", 256, 1), ("hbm4w_1perCU", 256, 2),
-                          ("hbm4w_2perCU", 512, 2)):
+    for name, C, mode in (("lds_1perCU", 256, 0), ("hbm_1perCU", 256, 1), ("tiles4w_1perCU", 256, 2),
+                          ("tiles4w_2perCU", 512, 2), ("hbm4w_2perCU", 512, 3)):
         chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=50000 + j, chain=10000 + j), model) for j in range(C)]
         for c in chains:
             assert tt.lib().tdt_chain_set_lds_mode(c.h, mode) == 0
