@@ -50,6 +50,7 @@ static_assert(kTilePts == 16, "a tile is one 16-lane DPP row (row_max_u64)");
 constexpr int kOrphanLds = 96;  // orphan records kept in LDS (more: read back from HBM)
 constexpr int kPre = 64 / kTilePts;  // LDS layout: hit tiles per wave whose points phase B preloads
 static_assert(kPre == 4, "the preload slots are four registers");
+constexpr int kCtmLds = 256;    // tiles in LDS, rays in HBM: hit tiles' candidate maxima kept in LDS
 constexpr int kListLds = 1024;  // rays in HBM: hit tiles / changed rays / hit super-tiles kept in LDS
 // Phase C leaves lanes idle (16 per hit tile, ~8 tiles): wave 7 lane 0 forms the decision's
 // phi_n-free parts; wave 6 lane 0 (LDS layout) begins the next proposal's guess -- its global loads
@@ -263,8 +264,9 @@ constexpr size_t kLdsBudget = 160 * 1024;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// small: the tiles in LDS (and, rays_lds, the per-ray arrays and the order too -- else those and the
-// hit tiles' candidate maxima stay in HBM: the 4-wave two-chains-per-CU kernel's "tiles" layout)
+// small: the tiles in LDS (and, rays_lds, the per-ray arrays and the order too -- else those stay in
+// HBM, and the first kCtmLds hit tiles' candidate maxima are in LDS: the 4-wave two-chains-per-CU
+// kernel's "tiles" layout)
 __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool small, int waves = kWaves,
                                             bool rays_lds = true) {
     LdsPlan L{};
@@ -281,7 +283,7 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
         L.tmaxd = o; o += align16(sizeof(double) * ntiles);
         L.tstart = o; o += align16(sizeof(int) * (ntiles + 1));
         L.thit = o; o += align16(sizeof(int) * (ntiles + 1));
-        if (rays_lds) { L.ctm = o; o += align16(sizeof(double) * (ntiles + 1)); }
+        L.ctm = o; o += align16(sizeof(double) * (rays_lds ? ntiles + 1 : kCtmLds));
         L.tray = o; o += align16(sizeof(int) * ntiles);
         if (rays_lds) {
             L.rayoff = o; o += align16(sizeof(int) * (n + 1));
@@ -321,7 +323,7 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
 // Views of the arrays a launch works on: LDS copies in SMALL mode, else HBM.
 struct Views {
     const float *tlo, *thi;
-    double *tmaxd, *ctm, *ptS, *prefix, *cptS, *cprefix, *term, *cterm;
+    double *tmaxd, *ptS, *prefix, *cptS, *cprefix, *term, *cterm;
     const double *tS, *sig;
     const int *tstart, *ray_off, *tray;
     int *thit, *rflag, *rhit, *ord;
@@ -331,6 +333,14 @@ struct Views {
     int rhit_cap;
     int4 *hrec;
     int hrec_cap;
+    // hit tile i's maximum if the proposal is accepted: the first ctm_cap in LDS (ctm), the rest in ctm_g
+    double *ctm, *ctm_g;
+    int ctm_cap;
+    __device__ __forceinline__ double ctm_at(int i) const { return i < ctm_cap ? ctm[i] : ctm_g[i]; }
+    __device__ __forceinline__ void ctm_put(int i, double x) const {
+        if (i < ctm_cap) ctm[i] = x;
+        else ctm_g[i] = x;
+    }
     __device__ __forceinline__ int ray_at(int i) const { return i < rhit_cap ? rhit[i] : rhit_g[i]; }
     __device__ __forceinline__ void ray_put(int i, int r) const {
         if (i < rhit_cap) rhit[i] = r;
@@ -849,7 +859,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     }
     v.term = d.term;
     v.cterm = d.cand_term;
-    v.ctm = d.tile_cmax;
+    v.ctm = v.ctm_g = d.tile_cmax;
+    v.ctm_cap = 0;
     if constexpr (SMALL && !RLDS) {  // the tiles only (the rays, the order, the candidate maxima in HBM)
         float *a = reinterpret_cast<float *>(lds + L.tlo), *b = reinterpret_cast<float *>(lds + L.thi);
         double *m = reinterpret_cast<double *>(lds + L.tmaxd);
@@ -866,6 +877,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         }
         v.tlo = a; v.thi = b; v.tmaxd = m; v.tstart = ts; v.tray = tr;
         v.thit = reinterpret_cast<int *>(lds + L.thit);
+        v.ctm = reinterpret_cast<double *>(lds + L.ctm);
+        v.ctm_cap = kCtmLds;
         __syncthreads();
     }
     if constexpr (RLDS) {
@@ -901,6 +914,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         v.cterm = reinterpret_cast<double *>(lds + L.cterm);
         v.thit = reinterpret_cast<int *>(lds + L.thit);
         v.ctm = reinterpret_cast<double *>(lds + L.ctm);
+        v.ctm_cap = NT + 1;
         v.rhit = reinterpret_cast<int *>(lds + L.rhit);
         v.rhit_cap = n;
         __syncthreads();  // ptS, tS, sig mirrored
@@ -1611,7 +1625,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 // round trip)
                 const int nt = sh.n_tiles;
                 constexpr int MU = 4, MS = (kWv >= 6 ? kWv - 4 : 1) * 64;
-                if constexpr (SMALL) {  // (~8 hit tiles: one item per thread)
+                if constexpr (RLDS) {  // (~8 hit tiles over 4 waves: one item per thread)
                     for (int i = tid - 128; i < nt * kTilePts; i += MS) {
                         const int sc = v.tile_rec(i / kTilePts).y;  // start << 5 | count
                         const int q = (sc >> 5) + (i % kTilePts);
@@ -1621,7 +1635,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             mk = (unsigned long long)__double_as_longlong(d.cand_flag[q] ? cd : bd);
                         }
                         mk = row_max_u64(mk);
-                        if ((i % kTilePts) == kTilePts - 1) v.ctm[i / kTilePts] = __longlong_as_double((long long)mk);
+                        if ((i % kTilePts) == kTilePts - 1) v.ctm_put(i / kTilePts, __longlong_as_double((long long)mk));
                     }
                 } else
                 for (int i0 = tid - 128; i0 < nt * kTilePts; i0 += MU * MS) {
@@ -1649,7 +1663,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         unsigned long long mk = 0ull;  // distances are >= 0: max as bit patterns
                         if (in[u]) mk = (unsigned long long)__double_as_longlong(cf[u] ? cd[u] : bd[u]);
                         mk = row_max_u64(mk);
-                        if ((i % kTilePts) == kTilePts - 1) v.ctm[i / kTilePts] = __longlong_as_double((long long)mk);
+                        if ((i % kTilePts) == kTilePts - 1) v.ctm_put(i / kTilePts, __longlong_as_double((long long)mk));
                     }
                 }
             }
@@ -1705,7 +1719,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         d.cand_flag[q] = 0;
                     }
                 if (fwd && action != tdchain::kChange) {
-                    for (int i = tid; i < nt; i += NTH) v.tmaxd[v.tile_rec(i).x] = v.ctm[i];
+                    for (int i = tid; i < nt; i += NTH) v.tmaxd[v.tile_rec(i).x] = v.ctm_at(i);
                     pend_sup = super_on;  // their super-tiles' maxima: at the top of the next iteration
                 }
                 for (int rr = tid; rr < nr; rr += NTH) {

@@ -14,11 +14,12 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from summarize import counters, mean, trace_rows  # noqa: E402
 
 ROWS = {  # traffic.json key -> (run, kernel name)
-    "k_chain_run/single": ("single", "k_chain_run<true, false>"),
-    "k_chain_run/many256": ("many", "k_chain_run<true, false>"),
+    "k_chain_run/single": ("single", "k_chain_run<true, false, 512, true>"),
+    "k_chain_run/many256": ("many", "k_chain_run<true, false, 512, true>"),
+    "k_chain_run/many512x2": ("packed", "k_chain_run<true, false, 256, false>"),
     "k_nn_tile/config3": ("single", "k_nn_tile<2>"),
     "k_nn_grid/config3": ("single", "k_nn_grid"),
-    "k_chain_run/stress": ("stress", "k_chain_run<false, false>"),
+    "k_chain_run/stress": ("stress", "k_chain_run<false, false, 512, false>"),
     "k_nn_grid4/stress": ("stress", "k_nn_grid4"),
     "k_nn_tile/stress": ("stress", "k_nn_tile<2>"),
     "k_raster_brute/section": ("aux", "k_raster_brute"),
