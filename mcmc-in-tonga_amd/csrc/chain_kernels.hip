@@ -1262,10 +1262,13 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                     }
             }
-            if (action == tdchain::kDeath) {  // deleteat! shift, staged before we know if it is accepted
+            if (RLDS && action == tdchain::kDeath) {  // deleteat! shift, staged before we know if it is accepted
                 const int sthr = query ? NTH - 64 : NTH;  // not the query wave: it starts at once
-                if (tid < sthr)
-                    for (int j = (int)p.index + 1 + tid; j < ncells; j += sthr) d.order_tmp[j] = v.ord[j];
+                // (the order in HBM: no staging -- an accepted death shifts it in phase G)
+                if constexpr (RLDS) {
+                    if (tid < sthr)
+                        for (int j = (int)p.index + 1 + tid; j < ncells; j += sthr) d.order_tmp[j] = v.ord[j];
+                }
             }
             if (query && wv == kWv - 1) {  // TD_inversion_function.jl:81 (birth), :146 (death)
                 const bool birth = action == tdchain::kBirth;
@@ -1734,8 +1737,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     pend_r = true;  // written at the top of the next iteration
                     if (wv == 1) delta_remark(v.term, v.prefix, v.cprefix, n, sh.dseg, smask, lane);
                 }
-                if (action == tdchain::kDeath && wv != 0) {  // deleteat!: positions after the killed one shift down
-                    constexpr int U = 4;                         // U loads in flight per thread
+                if (RLDS && action == tdchain::kDeath && wv != 0) {  // deleteat!: positions after the killed one shift down
+                    constexpr int U = 4;                                 // U loads in flight per thread
                     for (int j0 = (int)pp.index + 1 + w; j0 < ncells; j0 += U * kW) {
                         int sl[U];
 #pragma unroll
@@ -1800,6 +1803,30 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         sh.phi = phi_r;
                     }
                 }
+                if constexpr (!RLDS) {
+                    // the order in HBM, an accepted death (block-uniform): deleteat! in place, the whole
+                    // block -- a round's loads, a barrier, its shifted stores (the next round reads
+                    // only positions past the ones this one writes); a barrier before wave 0 reads
+                    // the shifted order for the next proposal
+                    if (action == tdchain::kDeath) {
+                        constexpr int U = 8;
+                        for (int b0 = (int)pp.index + 1; b0 < ncells; b0 += U * NTH) {
+                            int sl[U];
+#pragma unroll
+                            for (int u = 0; u < U; ++u) sl[u] = gload(v.ord + min(b0 + tid + u * NTH, ncells - 1));
+                            __syncthreads();
+#pragma unroll
+                            for (int u = 0; u < U; ++u) {
+                                const int j = b0 + tid + u * NTH;
+                                if (j < ncells) {
+                                    v.ord[j - 1] = sl[u];
+                                    d.rank[sl[u]] = j - 1;
+                                }
+                            }
+                        }
+                        __syncthreads();
+                    }
+                }
             } else {  // rejected: flags down, the changed rays get their old chi^2 terms back
                 if (wv != 0)
                     for (int c = w; c < nc; c += kW) d.cand_flag[d.changed[c]] = 0;
@@ -1843,8 +1870,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         cur_r ^= 1;  // adopt the guess: no copy
                         sh.cur = cur_r;
                     } else {
-                        // a just-killed position: later positions read the pre-shift order
-                        const int killed = (acc && action == tdchain::kDeath) ? (int)pp.index : -1;
+                        // a just-killed position: later positions read the pre-shift order (LDS
+                        // layout; in the HBM order phase G has shifted it already)
+                        const int killed = (RLDS && acc && action == tdchain::kDeath) ? (int)pp.index : -1;
                         auto slot_at = [&](int pos) {
                             return (killed >= 0 && pos >= killed) ? d.order_tmp[pos + 1] : v.ord[pos];
                         };

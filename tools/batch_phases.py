@@ -35,6 +35,7 @@ def main():
         o = (ctypes.c_int64 * 80)()
         L.tdt_chain_profile(c.h, 1, o)
         outs0.append(np.array(o[:], dtype=np.float64))
+    prop0 = np.array([c.stats()["proposed"] for c in chains], dtype=np.float64).sum(0)
     t0 = time.perf_counter()
     tt.run_batch(chains, iters)
     el = time.perf_counter() - t0
@@ -43,6 +44,13 @@ def main():
         o = (ctypes.c_int64 * 80)()
         L.tdt_chain_profile(c.h, 0, o)
         tot += np.array(o[:], dtype=np.float64) - o0
+    prop = np.array([c.stats()["proposed"] for c in chains], dtype=np.float64).sum(0) - prop0
+    # per action (birth, death, change, move): stamped phase cycles per proposal of that action
+    by_action = {}
+    for a, name in enumerate(("birth", "death", "change", "move")):
+        row = tot[16 + 10 * a: 16 + 10 * a + 9] / max(prop[a], 1)
+        by_action[name] = {"share": round(prop[a] / max(prop.sum(), 1), 3),
+                           **{p: round(x, 1) for p, x in zip(("top", "B", "C", "D", "E", "F", "G12", "G13", "G"), row)}}
     cyc = tot[:7].copy()
     cyc[6] += tot[12] + tot[13]
     n = C * iters
@@ -54,7 +62,7 @@ def main():
                       # per launch, averaged over the chains: preamble (mirrors, terms, draws) and epilogue
                       "preamble cycles per launch": round(tot[76] / max(tot[78], 1), 1),
                       "epilogue cycles per launch": round(tot[77] / max(tot[78], 1), 1),
-                      "launches": int(tot[78] / C)}, indent=1))
+                      "launches": int(tot[78] / C), "by_action": by_action}, indent=1))
 
 
 if __name__ == "__main__":
