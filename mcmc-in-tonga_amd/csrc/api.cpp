@@ -222,7 +222,7 @@ void free_ctx(td_ctx *c) {
     c->timer.release();
     void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->g.done, c->cells,
                    c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->phi,
-                   c->q, c->q_i, c->q_z, c->chain_desc, c->nn.g_count, c->nn.g_ent, c->raster, c->raster_i, c->raster_off,
+                   c->q, c->q_i, c->q_z, c->chain_desc, c->draws, c->nn.g_count, c->nn.g_ent, c->raster, c->raster_i, c->raster_off,
                    c->mf_dev};
     for (void *p : dev)
         if (p) (void)hipFree(p);

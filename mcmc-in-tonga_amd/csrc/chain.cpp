@@ -892,7 +892,8 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
         if (e != hipSuccess) return hip_err(ch->ctx, e, "chain descriptor upload");
         ch->desc_dirty = false;
     }
-    e = chain_run(&ch->dev, ch->dev_ptr, 1, iterations, ch->ctx->stream);
+    e = chain_run(&ch->dev, ch->dev_ptr, 1, iterations, ch->ctx->stream, nullptr,
+                  DrawsBuf{&ch->ctx->draws, &ch->ctx->draws_bytes});
     if (tm) tm->end("chain_run", t0, ch->ctx->stream);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "k_chain_run launch");
     e = hipStreamSynchronize(ch->ctx->stream);  // the kernel wrote the scalars to st_host
@@ -941,7 +942,8 @@ int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterati
     Timer *tm = c->timer.on ? &c->timer : nullptr;
     hipEvent_t t0 = tm ? tm->begin(c->stream) : nullptr;
     TD_HIP(c, hipMemcpyAsync(c->chain_desc, hd, bytes, hipMemcpyHostToDevice, c->stream));
-    hipError_t e = chain_run(hd, static_cast<const DevChain *>(c->chain_desc), (int)nchains, iterations, c->stream);
+    hipError_t e = chain_run(hd, static_cast<const DevChain *>(c->chain_desc), (int)nchains, iterations, c->stream,
+                             nullptr, DrawsBuf{&c->draws, &c->draws_bytes});
     if (tm) tm->end("chain_run", t0, c->stream);
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (batch)");
     TD_HIP(c, hipStreamSynchronize(c->stream));  // every chain wrote its scalars to its st_host

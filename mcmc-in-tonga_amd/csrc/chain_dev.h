@@ -175,6 +175,16 @@ struct ScriptArgs {
     double *out;
     Mailbox *mb;   // server mode (device address of pinned host memory)
     RoundBox *rb;  // resident tempering rounds (device address of pinned host memory), free-running chains
+    // a free-running launch of known length: every iteration's draws precomputed by k_draws
+    // (chain b's iteration iter0 + i at pre[b * pre_stride + i]); null: drawn in the kernel
+    const tdchain::Draws *pre;
+    long long pre_stride;
+};
+
+// Device scratch a launch may grow (owned by the context): the precomputed draws.
+struct DrawsBuf {
+    void **p;
+    size_t *bytes;
 };
 
 // Build the cache from scratch for the cells currently in slots 0..ncells-1
@@ -184,7 +194,7 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
 // (workgroup b runs chain b).  `host` = the descriptors, `dev` = their device
 // copy, contiguous (the kernel reads its fields from global memory).
 hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s,
-                     const ScriptArgs *script = nullptr);
+                     const ScriptArgs *script = nullptr, DrawsBuf db = DrawsBuf{nullptr, nullptr});
 // Testing: the chain's chi^2 code on a caller-given ptS (n <= 4096) --
 // path 2: k_chi2_prefix (the starting state's sequential prefix sums, what
 // chain_full_state runs), 3: the proposal-time sum (the terms of MCsub.jl:171,

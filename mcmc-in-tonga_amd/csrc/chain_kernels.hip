@@ -261,6 +261,7 @@ struct LdsPlan {
 };
 
 constexpr size_t kLdsBudget = 160 * 1024;
+constexpr size_t kDrawsBudget = (size_t)256 << 20;  // precomputed draws of one launch, at most (chain_run)
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -994,7 +995,11 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     // the draws (and their normal quantiles) of 64 iterations, one lane each:
     // a function of (seed, chain, iteration) only; and the first proposal
     if (wv == 0) {
-        if (!nscript) draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
+        if (sa.pre) {  // precomputed (k_draws): one round of loads
+            if (lane < iters) draws[lane] = sa.pre[(long long)bchain * sa.pre_stride + lane];
+        } else if (!nscript) {
+            draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(sh.iter + lane));
+        }
         wave_sync_lds();
         if (mb) {  // the first command (no proposal pending yet)
             if (lane == 0) {
@@ -1856,7 +1861,11 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             if (it + 1 < iters && !((mb || rbx) && sh.srv_quit)) {
                 if (((it + 1) & 63) == 0 && !nscript) {
                     wave_sync_lds();
-                    draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(iter0 + it + 1 + lane));
+                    if (sa.pre) {
+                        if (it + 1 + lane < iters) draws[lane] = sa.pre[(long long)bchain * sa.pre_stride + it + 1 + lane];
+                    } else {
+                        draws[lane] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(iter0 + it + 1 + lane));
+                    }
                     wave_sync_lds();
                 }
                 if (lane == 0) {
@@ -2122,11 +2131,48 @@ void chain_lds_sizes(const DevChain &d, int64_t out[4]) {
     out[3] = (int64_t)(a.total <= kLdsBudget && d.lds_mode != 1);  // the layout a launch takes: 1 = LDS
 }
 
+// Every iteration's draws of a launch (a function of seed, chain, iteration: tdchain::draw_iteration),
+// one thread each, ahead of k_chain_run: its per-64-iteration refill -- one wave computing 64 draws'
+// quantiles and logarithm on the chain's critical path -- becomes one round of loads.
+__global__ __launch_bounds__(256) void k_draws(const DevChain *__restrict__ dptr, long long iters,
+                                               tdchain::Draws *__restrict__ out) {
+    const DevChain &d = dptr[blockIdx.y];
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= iters) return;
+    out[(long long)blockIdx.y * iters + i] = tdchain::draw_iteration(d.seed, d.chain, (uint64_t)(d.st->iter + i));
+}
+
 hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s,
-                     const ScriptArgs *script) {
+                     const ScriptArgs *script, DrawsBuf db) {
     ScriptArgs sa{};
     if (script) sa = *script;
     sa.pin = -1;
+    sa.pre = nullptr;
+    sa.pre_stride = 0;
+    static const bool pre_env = [] {  // diagnostic: TD_PRE_DRAWS=0 keeps the in-kernel draws
+        const char *e = std::getenv("TD_PRE_DRAWS");
+        return !(e && e[0] == '0');
+    }();
+    const bool resident = sa.n > 0 || sa.mb != nullptr || sa.rb != nullptr;
+    const size_t pre_bytes = sizeof(tdchain::Draws) * (size_t)nchains * (size_t)std::max<int64_t>(iters, 0);
+    if (pre_env && db.p && !resident && iters > 0 && pre_bytes <= kDrawsBudget) {
+        if (pre_bytes > *db.bytes) {
+            if (*db.p) {
+                hipError_t e = hipStreamSynchronize(s);
+                if (e != hipSuccess) return e;
+                (void)hipFree(*db.p);
+                *db.p = nullptr;
+                *db.bytes = 0;
+            }
+            hipError_t e = hipMalloc(db.p, pre_bytes);
+            if (e != hipSuccess) return e;
+            *db.bytes = pre_bytes;
+        }
+        hipLaunchKernelGGL(k_draws, dim3((unsigned)((iters + 255) / 256), (unsigned)nchains), dim3(256), 0, s, dev,
+                           (long long)iters, static_cast<tdchain::Draws *>(*db.p));
+        sa.pre = static_cast<const tdchain::Draws *>(*db.p);
+        sa.pre_stride = iters;
+    }
     static const int pin_env = [] {
         const char *e = std::getenv("TD_XCC_PIN");
         return e ? std::atoi(e) : -1;

@@ -65,6 +65,8 @@ struct td_ctx {
     void *chain_desc = nullptr;         // device array of chain descriptors (td_chain_run_batch)
     size_t chain_desc_bytes = 0;
     void *h_chain_desc = nullptr;       // pinned staging of the same
+    void *draws = nullptr;              // k_chain_run: the launch's draws, precomputed (chain_run)
+    size_t draws_bytes = 0;
     tdstar::td_shadow *shadow = nullptr;  // td_evaluate's incremental path (incremental.cpp)
     int incremental = 2;                // 0 full evaluates; 1 one launch per call; 2 a resident server (tdt_set_incremental)
     // td_misfit: device copies of the last (tS, sig) given and a pinned [ptS | phi] staging area
