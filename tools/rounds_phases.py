@@ -41,11 +41,16 @@ def main():
         b = [(ctypes.c_int64 * 80)() for _ in chains]
         for c, x in zip(chains, b):
             L.tdt_chain_profile(c.h, 0, x)
-        cyc = np.mean([[float(y[k] - x[k]) for k in range(14)] for x, y in zip(a, b)], axis=0) / (rounds * K)
+        per = np.array([[float(y[k] - x[k]) for k in range(14)] for x, y in zip(a, b)]) / (rounds * K)
+        cyc = per.mean(axis=0)
+        # each replica's own work per proposal (every stamped phase but the round wait's slot 13)
+        work = per[:, [0, 1, 2, 3, 4, 5, 6, 12]].sum(axis=1)
         out[K] = {"us_per_round": round(el / rounds * 1e6, 2), "us_per_proposal_step": round(el / rounds / K * 1e6, 3),
                   "cycles_per_iter": {n: round(cyc[k], 1) for k, n in
                                       [(0, "top"), (1, "B"), (2, "C"), (3, "D"), (4, "E"), (5, "F"), (12, "G commit"),
-                                       (13, "G next + round wait"), (6, "final barrier")]}}
+                                       (13, "G next + round wait"), (6, "final barrier")]},
+                  "work_cycles_per_iter_by_replica": [round(w, 1) for w in work],
+                  "wait_cycles_per_iter_by_replica": [round(w, 1) for w in per[:, 13]]}
         for c in chains:
             c.close()
     print(json.dumps(out, indent=1))
