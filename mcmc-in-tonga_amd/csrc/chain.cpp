@@ -15,6 +15,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <new>
 #include <string>
@@ -68,9 +69,19 @@ struct td_rounds {
     hipStream_t stream = nullptr;
     bool running = false;
     long long seq = 0;
+    double tr_first = 0.0, tr_last = 0.0;  // diagnostic (TD_ROUNDS_TRACE): summed arrival times, rounds
+    long long tr_n = 0;
 };
 
 namespace {
+
+bool rounds_trace() {
+    static const bool on = [] {
+        const char *e = std::getenv("TD_ROUNDS_TRACE");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 
 int chain_err(td_chain *ch, int code, const std::string &m) { return set_err(ch ? ch->ctx : nullptr, code, m); }
 
@@ -700,6 +711,32 @@ int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out)
         *vol(&b->seq) = sq;
         bool lost = false;
         const auto t0 = std::chrono::steady_clock::now();
+        if (rounds_trace()) {  // diagnostic: when each replica's round ends, from the post (TD_ROUNDS_TRACE)
+            double first = -1.0, last = 0.0;
+            int left = nc;
+            std::vector<char> seen((size_t)nc, 0);
+            for (long long spin = 0; left > 0 && !lost; ++spin) {
+                for (int k = 0; k < nc; ++k) {
+                    if (seen[(size_t)k]) continue;
+                    if (*vol(&b->slot[k].done) == sq) {
+                        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+                        if (first < 0.0) first = us;
+                        last = us;
+                        seen[(size_t)k] = 1;
+                        --left;
+                    } else if (*vol(&b->slot[k].exited)) {
+                        lost = true;
+                    }
+                }
+                if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+                    return set_err(r->ctx, TD_ERR_HIP, "tempering rounds: no answer in 60 s");
+            }
+            if (!lost) {
+                r->tr_first += first;
+                r->tr_last += last;
+                r->tr_n += 1;
+            }
+        }
         for (int k = 0; k < nc && !lost; ++k)
             for (long long spin = 0;; ++spin) {
                 if (*vol(&b->slot[k].done) == sq) break;
@@ -798,6 +835,9 @@ int td_rounds_temper(td_rounds *r, int64_t M, int64_t K, const double *temps, in
 
 int td_rounds_destroy(td_rounds *r) {
     if (!r) return TD_OK;
+    if (rounds_trace() && r->tr_n > 0)
+        std::fprintf(stderr, "[rounds_trace] %d replicas, %lld rounds: first done %.2f us, last done %.2f us after the post\n",
+                     (int)r->chains.size(), (long long)r->tr_n, r->tr_first / r->tr_n, r->tr_last / r->tr_n);
     int rc = rounds_stop(r);
     for (td_chain *ch : r->chains) ch->rounds = nullptr;
     if (r->stream) (void)hipStreamDestroy(r->stream);

@@ -710,9 +710,13 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
 // Results in sh.rK / sh.rT / sh.rinv2t / sh.srv_quit.
 __device__ void round_wait(RoundBox *rb, int b, Shared &sh, int lane, bool publish, double phi) {
     RoundSlot *slot = &rb->slot[b];
+    // The mailbox is coherent pinned host memory and every access to it is a system-scope atomic,
+    // so no system-scope fence is needed -- one would write back (release) or invalidate (acquire)
+    // this XCD's whole L2, the chain's working set, at every round.  phi is acknowledged before
+    // done is written (the host reads done, then phi).
     if (publish && lane == 0) {
         mb_store(reinterpret_cast<long long *>(&slot->phi), __double_as_longlong(phi));
-        __threadfence_system();
+        __builtin_amdgcn_s_waitcnt(0);
         mb_store(&slot->done, sh.rseq);
     }
     const long long seen = sh.rseq;
@@ -720,15 +724,18 @@ __device__ void round_wait(RoundBox *rb, int b, Shared &sh, int lane, bool publi
     while (true) {
         const long long sq = mb_load(&rb->seq);
         if (sq != seen) {
-            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (lane == 0) {
+                // (the host wrote them before seq: three loads in flight together)
                 const long long w = mb_load(reinterpret_cast<const long long *>(rb) + 1);  // cmd | K << 32
+                const long long tb = mb_load(reinterpret_cast<const long long *>(&slot->T));
+                const long long ib = mb_load(reinterpret_cast<const long long *>(&slot->inv_2t));
                 const int cmd = (int)(w & 0xffffffffll), K = (int)(w >> 32);
                 sh.rseq = sq;
                 if (cmd == kRoundRun && K > 0) {
                     sh.rK = K;
-                    sh.rT = __longlong_as_double(mb_load(reinterpret_cast<const long long *>(&slot->T)));
-                    sh.rinv2t = __longlong_as_double(mb_load(reinterpret_cast<const long long *>(&slot->inv_2t)));
+                    sh.rT = __longlong_as_double(tb);
+                    sh.rinv2t = __longlong_as_double(ib);
                     sh.srv_quit = 0;
                 } else {
                     sh.srv_quit = 1;
