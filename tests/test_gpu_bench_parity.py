@@ -10,6 +10,8 @@ MCsub.jl:123-185) and against from-scratch evaluates of the chain's model.
 * many_chains: 256 chains (seeds 50000 + j) x 4 launches of 5000 in one
   td_chain_run_batch each; 4 sampled chains == their solo td_chain_run and
   == the HOST engine, final state == full evaluate;
+* many_chains_2per_cu: 512 of those chains two per CU (lds_mode 2), 4
+  launches of 5000; sampled chains == the same chains alone (8-wave kernel).
 * the stress chain (config 5): 10k synthetic rays x 20k cells, 200 + 2000
   proposals, DEVICE == HOST, final state == full evaluate;
 * the drop-in leg: the DROPIN engine (public td_evaluate per proposal, its
@@ -94,6 +96,33 @@ def test_many_chains_batch_follows_solo_and_host(tt, ds, ctx):
         assert same_models(m, solo.model()) and same_models(m, host.model())
         solo.close()
         host.close()
+    for c in chains:
+        c.close()
+
+
+@pytest.mark.timeout(600)
+def test_many_chains_two_per_cu_follow_solo(tt, ds, ctx):
+    """bench.py's many_chains_2per_cu leg: 512 config-3 chains (seeds 50000 + j)
+    in the 4-wave tiles-in-LDS kernel, two per CU (lds_mode 2), 4 launches of
+    5000; sampled chains equal the same chains run alone in the 8-wave kernel,
+    and their state equals a full evaluate."""
+    prm = tt.define_TDstructrure().replace(max_cells=2 * 5000)
+    model = tt.random_model(5000, 3)
+    C = 512
+    chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=50000 + j, chain=10000 + j), model) for j in range(C)]
+    for c in chains:
+        assert tt.lib().tdt_chain_set_lds_mode(c.h, 2) == 0
+    launches = 4  # bench: one warm-up launch + 3 timed
+    for _ in range(launches):
+        tt.run_batch(chains, BENCH_ITERS)
+    for j in (0, 131, 300, 511):
+        solo = tt.Chain(ctx, tt.chain_params(prm, ds, seed=50000 + j, chain=10000 + j), model)
+        for _ in range(launches):
+            solo.run(BENCH_ITERS)
+        agree(chains[j], solo)
+        m = state_is_full_evaluate(ctx, chains[j])
+        assert same_models(m, solo.model())
+        solo.close()
     for c in chains:
         c.close()
 
