@@ -51,7 +51,12 @@ constexpr int kOrphanLds = 96;  // orphan records kept in LDS (more: read back f
 constexpr int kPre = 64 / kTilePts;  // LDS layout: hit tiles per wave whose points phase B preloads
 static_assert(kPre == 4, "the preload slots are four registers");
 constexpr int kCtmLds = 256;    // tiles in LDS, rays in HBM: hit tiles' candidate maxima kept in LDS
-constexpr int kListLds = 1024;  // rays in HBM: hit tiles / changed rays / hit super-tiles kept in LDS
+constexpr int kListLds = 1024;
+// LDS layout, phase D: from this many orphans on, one search for all of them (the bucket region
+// around them staged once in LDS, a thread per orphan) instead of one wave's grid search each
+constexpr int kBatchOrphans = 64;
+constexpr int kBatchCand = 192;     // cell entries staged (phase E's idle ray scratch: 28 B each)
+constexpr int kBatchBuckets = 512;  // buckets in the region at most  // rays in HBM: hit tiles / changed rays / hit super-tiles kept in LDS
 // Phase C leaves lanes idle (16 per hit tile, ~8 tiles): wave 7 lane 0 forms the decision's
 // phi_n-free parts; wave 6 lane 0 (LDS layout) begins the next proposal's guess -- its global loads
 // fly across the phase barriers until phase F finishes it there
@@ -202,6 +207,7 @@ struct Shared {
     double phi_lo, phi_hi, b_lo, b_hi;
     int accept;
     int n_tiles, n_changed, n_orphans, n_rays, k0;
+    int ob_lo[3], ob_hi[3], ob_ncand, ob_nfb;  // phase D's orphan-batch search (LDS layout)
     int n_super[2];  // rays in HBM: super-tiles hit, by iteration parity (the next iteration refreshes their maxima)
     int pts_seen, ray_pts;
     // bucket-grid update of an accepted proposal (applied by the last wave in phase G)
@@ -1379,7 +1385,149 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 // ========= phase D: re-search orphaned points, one wave each =========
                 no = sh.n_orphans;
                 const bool death = action == tdchain::kDeath;
-                for (int o = wv; o < no; o += kWv) {  // one wave per orphan, no block barrier
+                const int skip_s = death ? slot_k : -1, moved_s = death ? -1 : slot_k;
+                // the orphans the per-wave search takes: all of them in order, or the batch's unproven ones
+                int nlist = no;
+                const int *olist = nullptr;
+                if constexpr (RLDS) {
+                    if (no >= kBatchOrphans && 2 * n >= no && sh.grid_ovf == 0) {  // (block-uniform)
+                        // The nearest cell of every orphan, at once: the buckets of the orphans' bucket
+                        // box grown by one on each side, their entries staged in LDS (phase E's ray
+                        // scratch is idle), then a thread per orphan over all of them, with the moved cell
+                        // at its new site.  Proven as the per-wave search proves: a distance strictly
+                        // below the region's faces (the region holds every orphan's 3x3x3 block), no tie
+                        // at the minimum; else the orphan goes to the per-wave search (its full scan).
+                        const CellGrid &G = d.grid;
+                        double *ex = reinterpret_cast<double *>(ray_scratch);
+                        double *ey = ex + kBatchCand, *ez = ey + kBatchCand;
+                        int *es = reinterpret_cast<int *>(ez + kBatchCand);
+                        int *fb = reinterpret_cast<int *>(v.cptS);  // (candidate t* of phase E: idle)
+                        auto orphan_xyz = [&](int o, double &qx, double &qy, double &qz) {
+                            if (o < kOrphanLds) {
+                                qx = sh.orph[o].x;
+                                qy = sh.orph[o].y;
+                                qz = sh.orph[o].z;
+                            } else {
+                                const int q = d.orphans[o];
+                                qx = d.px[q];
+                                qy = d.py[q];
+                                qz = d.pz[q];
+                            }
+                        };
+                        if (tid == 0) {
+                            for (int a3 = 0; a3 < 3; ++a3) {
+                                sh.ob_lo[a3] = INT_MAX;
+                                sh.ob_hi[a3] = -1;
+                            }
+                            sh.ob_ncand = sh.ob_nfb = 0;
+                        }
+                        __syncthreads();
+                        for (int o = tid; o < no; o += NTH) {
+                            double qx, qy, qz;
+                            orphan_xyz(o, qx, qy, qz);
+                            const int bi = grid_axis(qx, G.x0, G.ix, G.gx), bj = grid_axis(qy, G.y0, G.iy, G.gy),
+                                      bk = grid_axis(qz, G.z0, G.iz, G.gz);
+                            atomicMin(&sh.ob_lo[0], bi);
+                            atomicMax(&sh.ob_hi[0], bi);
+                            atomicMin(&sh.ob_lo[1], bj);
+                            atomicMax(&sh.ob_hi[1], bj);
+                            atomicMin(&sh.ob_lo[2], bk);
+                            atomicMax(&sh.ob_hi[2], bk);
+                        }
+                        __syncthreads();
+                        const int i0 = max(sh.ob_lo[0] - 1, 0), i1 = min(sh.ob_hi[0] + 1, G.gx - 1);
+                        const int j0 = max(sh.ob_lo[1] - 1, 0), j1 = min(sh.ob_hi[1] + 1, G.gy - 1);
+                        const int k0b = max(sh.ob_lo[2] - 1, 0), k1b = min(sh.ob_hi[2] + 1, G.gz - 1);
+                        const int nbx = i1 - i0 + 1, nby = j1 - j0 + 1, nbz = k1b - k0b + 1;
+                        if (nbx * nby * nbz <= kBatchBuckets) {
+                            for (int b = tid; b < nbx * nby * nbz; b += NTH) {
+                                const int bucket = ((k0b + b / (nbx * nby)) * G.gy + (j0 + (b / nbx) % nby)) * G.gx +
+                                                   (i0 + b % nbx);
+                                const int cnt = d.bucket_count[bucket];
+                                const int base = cnt > 0 ? atomicAdd(&sh.ob_ncand, cnt) : 0;
+                                for (int e = 0; e < cnt && base + e < kBatchCand; ++e) {
+                                    const BucketEntry &be = d.buckets[bucket * kBucketCap + e];
+                                    ex[base + e] = be.x;
+                                    ey[base + e] = be.y;
+                                    ez[base + e] = be.z;
+                                    es[base + e] = be.slot;
+                                }
+                            }
+                            __syncthreads();
+                            const int nc = sh.ob_ncand;
+                            if (nc <= kBatchCand) {
+                                // four lanes per orphan (a quad), each over a quarter of the entries,
+                                // then the quad's lexicographic minimum (the loop is wave-uniform)
+                                for (int o0 = 0; o0 < no; o0 += NTH / 4) {
+                                    const int o = o0 + tid / 4, part = tid & 3;
+                                    const bool act = o < no;
+                                    double qx = 0.0, qy = 0.0, qz = 0.0;
+                                    if (act) orphan_xyz(o, qx, qy, qz);
+                                    double bd = kSentinel;
+                                    int bs = -1;
+                                    bool tie = false;
+                                    auto take = [&](double dd, int sl) {
+                                        if (dd < bd) {
+                                            bd = dd;
+                                            bs = sl;
+                                            tie = false;
+                                        } else if (dd == bd && dd < kSentinel) {
+                                            tie = true;
+                                        }
+                                    };
+                                    for (int c = part; c < nc; c += 4) {
+                                        const int sl = es[c];
+                                        const double dd = dist2(ex[c], ey[c], ez[c], qx, qy, qz);
+                                        if (sl != skip_s && sl != moved_s) take(dd, sl);
+                                    }
+                                    if (moved_s >= 0 && part == 0)  // the moved cell, at its proposed site
+                                        take(dist2(pp.x, pp.y, pp.z, qx, qy, qz), moved_s);
+#pragma unroll
+                                    for (int m = 1; m <= 2; m <<= 1) {  // quad reduction (distinct slots per lane)
+                                        const double od = __shfl_xor(bd, m, 4);
+                                        const int os = __shfl_xor(bs, m, 4);
+                                        const bool ot = __shfl_xor((int)tie, m, 4) != 0;
+                                        if (od < bd) {
+                                            bd = od;
+                                            bs = os;
+                                            tie = ot;
+                                        } else if (od == bd && od < kSentinel) {
+                                            tie = true;
+                                        }
+                                    }
+                                    if (!act || part != 0) continue;
+                                    // every cell outside the region lies beyond one of its inner faces
+                                    double lb = __builtin_huge_val();
+                                    auto face = [&lb](double w, double w0, double h, double e, int g, int lo, int hi) {
+                                        if (lo > 0) {
+                                            const double gap = (w - (w0 + (double)lo * h)) - e;
+                                            lb = gap > 0.0 ? (gap * gap < lb ? gap * gap : lb) : 0.0;
+                                        }
+                                        if (hi < g - 1) {
+                                            const double gap = ((w0 + (double)(hi + 1) * h) - w) - e;
+                                            lb = gap > 0.0 ? (gap * gap < lb ? gap * gap : lb) : 0.0;
+                                        }
+                                    };
+                                    face(qx, G.x0, G.hx, G.ex, G.gx, i0, i1);
+                                    face(qy, G.y0, G.hy, G.ey, G.gy, j0, j1);
+                                    face(qz, G.z0, G.hz, G.ez, G.gz, k0b, k1b);
+                                    if (bs >= 0 && bd < kSentinel && !tie && bd < lb) {
+                                        const int q = o < kOrphanLds ? sh.orph[o].q : d.orphans[o];
+                                        const int ray = o < kOrphanLds ? sh.orph[o].ray : d.pt_ray[q];
+                                        mark(d, v, sh, q, ray, bs, bd, d.czeta[bs]);
+                                    } else {
+                                        fb[atomicAdd(&sh.ob_nfb, 1)] = o;
+                                    }
+                                }
+                                __syncthreads();
+                                nlist = sh.ob_nfb;
+                                olist = fb;
+                            }
+                        }
+                    }
+                }
+                for (int k = wv; k < nlist; k += kWv) {  // one wave per orphan, no block barrier
+                    const int o = olist ? olist[k] : k;
                     double qx, qy, qz;
                     int q, ray;
                     if (o < kOrphanLds) {
@@ -1395,11 +1543,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         qz = d.pz[q];
                         ray = d.pt_ray[q];
                     }
-                    const Nearest r = wave_nearest(d, v, sh, lane, qx, qy, qz, death ? slot_k : -1,
-                                                   death ? -1 : slot_k, pp.x, pp.y, pp.z);
+                    const Nearest r = wave_nearest(d, v, sh, lane, qx, qy, qz, skip_s, moved_s, pp.x, pp.y, pp.z);
                     if (lane == 0) mark(d, v, sh, q, ray, r.s, r.d, r.z);
                 }
-                if (no > 0) __syncthreads();
+                if (nlist > 0) __syncthreads();
                 STAMP(3);
                 // ================= phase E: t* of the rays that changed =================
                 const int nr = sh.n_rays;
