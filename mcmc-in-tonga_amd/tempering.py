@@ -137,7 +137,11 @@ class TemperingLadder:
                                             for c in self.chains)
         # DEVICE td_chain replicas of one context: one launch resident across the rounds (td_rounds),
         # the temperatures posted to it every round instead of a launch per round
-        self.resident = bool(resident) and self.local >= 1 and all(
+        # -- but not when the gather is a GPU collective (RCCL, world > 1): the resident kernel spins
+        # between rounds, and with few hardware queues per process (GPU_MAX_HW_QUEUES) the collective's
+        # kernel could queue behind it until its idle watchdog; a launch per round then (same trace)
+        gpu_collective = self.ex.world > 1 and str(getattr(self.ex, "device", "cpu")).startswith("cuda")
+        self.resident = bool(resident) and not gpu_collective and self.local >= 1 and all(
             hasattr(c, "h") and getattr(c, "ctx", None) is self.chains[0].ctx and
             getattr(getattr(c, "params", None), "engine", None) == 0 for c in self.chains)
         self.rounds = None

@@ -169,3 +169,30 @@ def test_native_swap_step_is_decide_swaps(tt):
     tl = tp.geometric_ladder(3)
     assert L.td_swap_decide(3, ph.ctypes.data_as(PD), bad.ctypes.data_as(P64), tl.ctypes.data_as(PD), 0,
                             ctypes.c_uint64(1), out.ctypes.data_as(P64), None, None) != 0
+
+
+def test_resident_rounds_not_under_a_gpu_collective():
+    """Resident rounds (one spinning launch) only when the gather is not an RCCL
+    collective: with few hardware queues the collective could wait behind it."""
+
+    class DeviceStandIn(ToyChain):
+        h, ctx = 1, "ctx"
+
+        class params:
+            engine = 0
+
+    class FakeDist:
+        def __init__(self, world):
+            self.w = world
+
+        def get_world_size(self):
+            return self.w
+
+        def get_rank(self):
+            return 0
+
+    chains = [DeviceStandIn(1), DeviceStandIn(2)]
+    assert tempering.TemperingLadder(chains).resident
+    assert tempering.TemperingLadder(chains, exchange=tempering.Exchange(FakeDist(2), "cpu")).resident
+    assert not tempering.TemperingLadder(chains, exchange=tempering.Exchange(FakeDist(2), "cuda:0")).resident
+    assert not tempering.TemperingLadder(chains, resident=False).resident
