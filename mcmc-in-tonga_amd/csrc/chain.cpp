@@ -983,7 +983,7 @@ int td_chain_run_batch(td_chain *const *chains, int64_t nchains, int64_t iterati
     hipEvent_t t0 = tm ? tm->begin(c->stream) : nullptr;
     TD_HIP(c, hipMemcpyAsync(c->chain_desc, hd, bytes, hipMemcpyHostToDevice, c->stream));
     hipError_t e = chain_run(hd, static_cast<const DevChain *>(c->chain_desc), (int)nchains, iterations, c->stream,
-                             nullptr, DrawsBuf{&c->draws, &c->draws_bytes});
+                             nullptr, DrawsBuf{&c->draws, &c->draws_bytes}, c->num_cus);
     if (tm) tm->end("chain_run", t0, c->stream);
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (batch)");
     TD_HIP(c, hipStreamSynchronize(c->stream));  // every chain wrote its scalars to its st_host

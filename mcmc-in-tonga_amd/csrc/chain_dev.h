@@ -194,7 +194,8 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
 // (workgroup b runs chain b).  `host` = the descriptors, `dev` = their device
 // copy, contiguous (the kernel reads its fields from global memory).
 hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s,
-                     const ScriptArgs *script = nullptr, DrawsBuf db = DrawsBuf{nullptr, nullptr});
+                     const ScriptArgs *script = nullptr, DrawsBuf db = DrawsBuf{nullptr, nullptr},
+                     int num_cus = 0);  // > 0: a batch of more chains than CUs packs two per CU
 // Testing: the chain's chi^2 code on a caller-given ptS (n <= 4096) --
 // path 2: k_chi2_prefix (the starting state's sequential prefix sums, what
 // chain_full_state runs), 3: the proposal-time sum (the terms of MCsub.jl:171,

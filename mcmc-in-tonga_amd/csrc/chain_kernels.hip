@@ -2297,7 +2297,7 @@ __global__ __launch_bounds__(256) void k_draws(const DevChain *__restrict__ dptr
 }
 
 hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int64_t iters, hipStream_t s,
-                     const ScriptArgs *script, DrawsBuf db) {
+                     const ScriptArgs *script, DrawsBuf db, int num_cus) {
     ScriptArgs sa{};
     if (script) sa = *script;
     sa.pin = -1;
@@ -2341,7 +2341,7 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
     size_t small = 0, big = 0, half = 0, hyb = 0;
     // packed: every chain asks for two chains per CU (lds_mode 2: the tiles in LDS when they fit; 3, testing:
     // the rays-in-HBM 4-wave kernel)
-    bool force_hbm = false, packed = true, tiles_ok = true;
+    bool force_hbm = false, packed = true, tiles_ok = true, all_auto = true;
     for (int b = 0; b < nchains; ++b) {
         const DevChain &d = host[b];
         small = std::max(small, lds_plan(d.ntiles, d.n, d.cap, true).total);
@@ -2351,8 +2351,18 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
         force_hbm = force_hbm || d.lds_mode >= 1;
         packed = packed && d.lds_mode >= 2;
         tiles_ok = tiles_ok && d.lds_mode == 2;
+        all_auto = all_auto && d.lds_mode == 0;
     }
     const bool scripted = sa.n > 0 || sa.mb != nullptr;
+    // More chains than CUs: one chain per CU would run them in rounds of num_cus workgroups; two
+    // 4-wave chains per CU run them all at once (1.35x the 8-wave kernel's rate at 512 config-3
+    // chains) -- the tiles-in-LDS kernel when it fits, else the all-in-HBM one
+    if (all_auto && num_cus > 0 && nchains > num_cus && !scripted && sa.rb == nullptr &&
+        (hyb <= kLdsBudget / 2 || half <= kLdsBudget / 2)) {
+        packed = true;
+        tiles_ok = hyb <= kLdsBudget / 2;
+        force_hbm = true;
+    }
     static bool attr_set = false;  // dynamic LDS above 64 KB needs the attribute (once per kernel)
     if (!attr_set) {
         for (const void *k : {(const void *)k_chain_run<true, false, kChainThreads>,

@@ -101,9 +101,11 @@ def test_many_chains_batch_follows_solo_and_host(tt, ds, ctx):
 
 
 @pytest.mark.timeout(600)
-def test_many_chains_two_per_cu_follow_solo(tt, ds, ctx):
+@pytest.mark.parametrize("knob", [True, False])
+def test_many_chains_two_per_cu_follow_solo(tt, ds, ctx, knob):
     """bench.py's many_chains_2per_cu leg: 512 config-3 chains (seeds 50000 + j)
-    in the 4-wave tiles-in-LDS kernel, two per CU (lds_mode 2), 4 launches of
+    in the 4-wave tiles-in-LDS kernel, two per CU (lds_mode 2; or, knob off, the
+    launcher's own choice for a batch of more chains than CUs), 4 launches of
     5000; sampled chains equal the same chains run alone in the 8-wave kernel,
     and their state equals a full evaluate."""
     prm = tt.define_TDstructrure().replace(max_cells=2 * 5000)
@@ -111,7 +113,8 @@ def test_many_chains_two_per_cu_follow_solo(tt, ds, ctx):
     C = 512
     chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=50000 + j, chain=10000 + j), model) for j in range(C)]
     for c in chains:
-        assert tt.lib().tdt_chain_set_lds_mode(c.h, 2) == 0
+        if knob:
+            assert tt.lib().tdt_chain_set_lds_mode(c.h, 2) == 0
     launches = 4  # bench: one warm-up launch + 3 timed
     for _ in range(launches):
         tt.run_batch(chains, BENCH_ITERS)
