@@ -318,8 +318,8 @@ def main():
         out["ingest_trilinear"] = ingest_trilinear(tt)
     if rank == 0 and a.batch_chains > 0:
         out["many_chains"] = many_chains(tt, ctx, ds, prm, model, a.batch_chains, a.batch_iters)
-        out["many_chains_2per_cu"] = many_chains(tt, ctx, ds, prm, model, 2 * a.batch_chains, a.batch_iters,
-                                                 lds_mode=2)
+        # more chains than CUs: td_chain_run_batch packs two per CU by itself
+        out["many_chains_2per_cu"] = many_chains(tt, ctx, ds, prm, model, 2 * a.batch_chains, a.batch_iters)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the host-core baseline: N = 1 only
         out["cpu_baseline"] = cpu_baseline(ds, model, a.cpu_seconds, tt if not a.no_full_evaluate else None)
         if out["cpu_baseline"]["value"] > 0:
@@ -451,12 +451,16 @@ def stress_chains(tt, dist, coll_dev, rank, world, device, iters):
 def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3, lds_mode=0):
     """Occupancy mode (SURVEY 7 / 8d "batched multi-chain streams"): C
     independent config-3 chains on this GPU, one workgroup each, one launch
-    per step.  lds_mode 2: two chains per CU (the 4-wave tiles-in-LDS kernel,
-    DESIGN.md 4.4).  Reported beside the headline, never as `value`."""
+    per step.  More chains than CUs: two per CU (the 4-wave tiles-in-LDS
+    kernel, the launcher's own choice; lds_mode 2 forces it).
+    Reported beside the headline, never as `value`."""
     chains = [tt.Chain(ctx, tt.chain_params(prm, ds, seed=50000 + j, chain=10000 + j), model) for j in range(C)]
     for c in chains:
         if lds_mode:
             tt.lib().tdt_chain_set_lds_mode(c.h, lds_mode)
+    import torch
+    # two chains per CU: forced (lds_mode 2), or the launcher's own choice for more chains than CUs
+    packed = lds_mode == 2 or (lds_mode == 0 and C > torch.cuda.get_device_properties(0).multi_processor_count)
     tt.run_batch(chains, iters)  # warmup
     b0 = sum(c.stats()["bytes"] for c in chains)
     ctx.timing(enable=True, reset=True)
@@ -473,8 +477,8 @@ def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3, lds_mode=0):
     avg_s = kms / 1e3 / max(launches, 1)
     roof = chain_roofline("k_chain_run (grid = %d chains)" % C, model_bytes(int(ctx.P), int(ctx.n), len(model.xCell)),
                           C * iters, avg_s, nbytes / max(launches, 1),
-                          "k_chain_run/many%d%s" % (C, "x2" if lds_mode == 2 else ""), iters == 5000)
-    return {"chains": C, "chains_per_cu": 2 if lds_mode == 2 else 1, "proposals_per_s": round(value, 1), "per_chain_proposals_per_s": round(value / C, 1),
+                          "k_chain_run/many%d%s" % (C, "x2" if packed else ""), iters == 5000)
+    return {"chains": C, "chains_per_cu": 2 if packed else 1, "proposals_per_s": round(value, 1), "per_chain_proposals_per_s": round(value / C, 1),
             "ms_per_launch": round(kms / max(launches, 1), 4), "iters_per_launch": iters, "roofline": roof}
 
 
