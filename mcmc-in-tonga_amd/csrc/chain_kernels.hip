@@ -651,7 +651,9 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
                 sh.srv_busy_w = (long long)wall_clock64();
                 mb_store(&mb->diag[2], polls);
             }
-            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            // (no system-scope acquire: the command is read through system-scope atomics, and one
+            // would invalidate this XCD's L2, the chain's working set, at every call)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             // the whole command in one round trip: one mailbox word per lane, into LDS
             if (lane < kWords) sh.mbox[lane] = mb_load(reinterpret_cast<const long long *>(mb) + lane);
             wave_sync_lds();
@@ -673,7 +675,7 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
                 }
                 if (lane == 0) {
                     mb_store(reinterpret_cast<long long *>(&mb->qval), __double_as_longlong(val));
-                    __threadfence_system();
+                    __builtin_amdgcn_s_waitcnt(0);  // the answer acknowledged before done (no L2 write-back)
                     mb_store(&mb->done, sq);
                 }
                 wave_sync_lds();
@@ -1839,25 +1841,29 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             if (nscript && sdec != 1 && wv == 0) {
                 // report phi_n and the changed rays' new ptS as [phi, k, (ray, ptS) x k] (the
                 // caller holds the model's ptS); k = -1: the whole proposed ptS follows
-                double *out = sa.out;
+                // (pinned host memory, written through system-scope stores: see below)
+                long long *out = reinterpret_cast<long long *>(sa.out);
+                auto put = [&](int i, double x) { mb_store(out + i, __double_as_longlong(x)); };
                 const bool few = 2 * nr + 2 <= n + 1;
                 if (few) {
                     for (int i = lane; i < nr; i += 64) {
                         const int r = v.ray_at(i);
-                        out[2 + 2 * i] = (double)r;
-                        out[3 + 2 * i] = v.cptS[r];
+                        put(2 + 2 * i, (double)r);
+                        put(3 + 2 * i, v.cptS[r]);
                     }
                 } else {
-                    for (int r = lane; r < n; r += 64) out[2 + r] = v.rflag[r] ? v.cptS[r] : v.ptS[r];
+                    for (int r = lane; r < n; r += 64) put(2 + r, v.rflag[r] ? v.cptS[r] : v.ptS[r]);
                 }
                 if (lane == 0) {
-                    out[0] = sh.phi_n;
-                    out[1] = few ? (double)nr : -1.0;
+                    put(0, sh.phi_n);
+                    put(1, few ? (double)nr : -1.0);
                 }
             }
             if (mb && sdec == kDecideLater) {  // answer the command, then its fate comes with the next one
                 if (wv == 0) {
-                    __threadfence_system();
+                    // the answer's system-scope stores acknowledged before done: no system-scope
+                    // fence, which would write back this XCD's L2 at every call
+                    __builtin_amdgcn_s_waitcnt(0);
                     wave_sync_lds();
                     if (lane == 0) mb_store(&mb->done, sh.srv_seq);
                     server_wait(mb, d, v, sh, lane);
