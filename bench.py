@@ -458,9 +458,8 @@ def many_chains(tt, ctx, ds, prm, model, C, iters, steps=3, lds_mode=0):
     for c in chains:
         if lds_mode:
             tt.lib().tdt_chain_set_lds_mode(c.h, lds_mode)
-    import torch
     # two chains per CU: forced (lds_mode 2), or the launcher's own choice for more chains than CUs
-    packed = lds_mode == 2 or (lds_mode == 0 and C > torch.cuda.get_device_properties(0).multi_processor_count)
+    packed = lds_mode == 2 or (lds_mode == 0 and C > ctx.num_cus)
     tt.run_batch(chains, iters)  # warmup
     b0 = sum(c.stats()["bytes"] for c in chains)
     ctx.timing(enable=True, reset=True)

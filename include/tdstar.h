@@ -67,6 +67,7 @@ typedef struct td_info {
     int64_t nsegments;    /* S = P - (rays with >= 1 point) */
     double likelihood;    /* the MCsub.jl:179 constant for the current allSig */
     char arch[32];        /* e.g. "gfx950" */
+    int32_t num_cus;      /* compute units: td_chain_run_batch packs two chains per CU beyond this many */
 } td_info;
 int td_get_info(const td_ctx *ctx, td_info *info);
 

@@ -30,7 +30,7 @@ _vp = ctypes.c_void_p
 
 class TdInfo(ctypes.Structure):
     _fields_ = [("abi_version", _i32), ("device", _i32), ("m", _i64), ("n", _i64), ("npoints", _i64),
-                ("nsegments", _i64), ("likelihood", _d), ("arch", ctypes.c_char * 32)]
+                ("nsegments", _i64), ("likelihood", _d), ("arch", ctypes.c_char * 32), ("num_cus", _i32)]
 
 
 class TdChainParams(ctypes.Structure):

@@ -384,6 +384,7 @@ int td_get_info(const td_ctx *ctx, td_info *info) {
     info->nsegments = ctx->g.P - nonempty;
     info->likelihood = ctx->likelihood;
     std::snprintf(info->arch, sizeof info->arch, "%s", ctx->arch.c_str());
+    info->num_cus = ctx->num_cus;
     return TD_OK;
 }
 

@@ -41,6 +41,7 @@ class TdContext:
         self.likelihood_const = float(info.likelihood)
         self.arch = info.arch.decode()
         self.device = int(info.device)
+        self.num_cus = int(info.num_cus)
 
     @classmethod
     def from_datastruct(cls, ds, device=-1):
