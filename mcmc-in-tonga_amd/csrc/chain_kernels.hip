@@ -1682,14 +1682,15 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                             // the sequential phi_n lies within (n - 1) ulps of the exact sum, far inside 1e-9
                             const double b_lo = (Sa - Ea) * (1.0 - 1e-9), b_hi = (Sa + Ea) * (1.0 + 1e-9);
-                            if (lane == 0) {
-                                const bool a_min = tdchain::accept_t(P, inv2t_r, pp, sh.phi_lo, b_hi, czeta, zeta_killed,
-                                                                     zetanew_death, sh.lnN);
-                                const bool a_max = tdchain::accept_t(P, inv2t_r, pp, sh.phi_hi, b_lo, czeta, zeta_killed,
-                                                                     zetanew_death, sh.lnN);
+                            {  // the two corners side by side: lane 0 (phi_lo, b_hi), lane 1 (phi_hi, b_lo)
+                                const bool lo = lane == 0;
+                                const int a = lane < 2 ? (int)tdchain::accept_t(P, inv2t_r, pp, lo ? sh.phi_lo : sh.phi_hi,
+                                                                               lo ? b_hi : b_lo, czeta, zeta_killed,
+                                                                               zetanew_death, sh.lnN)
+                                                       : 0;
+                                const int a_min = __builtin_amdgcn_readlane(a, 0), a_max = __builtin_amdgcn_readlane(a, 1);
                                 bdec = a_min != a_max ? 0 : a_min ? 2 : 1;
                             }
-                            bdec = __builtin_amdgcn_readfirstlane(bdec);
                             // a tempering round's last iteration publishes phi: decided exactly (and
                             // every sum made exact) whatever the bounds say (testing: every k-th too)
                             if (rbx && it + 1 == round_end) bdec = 0;
