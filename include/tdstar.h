@@ -31,7 +31,8 @@
 extern "C" {
 #endif
 
-#define TDSTAR_ABI_VERSION 1
+/* 2: td_info gained num_cus (its size changed) */
+#define TDSTAR_ABI_VERSION 2
 
 typedef struct td_ctx td_ctx;
 typedef struct td_chain td_chain;

@@ -266,3 +266,17 @@ def test_acceptance_matches_reference_formulas(tt):
                 got = L.tdt_accept(ctypes.byref(prm), action, u, zn, N, phi, phi_n, cz, zk, zd)
                 assert got == (1 if u < a else 0), (prior, action, a, u)
 
+
+
+def test_td_info_layout_matches_header():
+    """td_info (include/tdstar.h) and the ctypes mirror agree: the ABI version and
+    the struct's size (num_cus appended in ABI 2)."""
+    import ctypes
+    import re
+
+    from mcmc_in_tonga_amd import _lib
+
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "tdstar.h")).read()
+    assert int(re.search(r"#define TDSTAR_ABI_VERSION (\d+)", hdr).group(1)) == 2
+    assert [f for f, _ in _lib.TdInfo._fields_][-1] == "num_cus"
+    assert ctypes.sizeof(_lib.TdInfo) == 4 + 4 + 8 * 4 + 8 + 32 + 4 + 4  # (tail padding to 8)
