@@ -357,7 +357,7 @@ def tempering_config4(tt, ctx, ds, nrep=8, ncells=2000, swap_every=10, rounds=30
            "rounds_by": "one resident k_chain_run launch; swap steps in the library between rounds "
                         "(td_rounds_temper, no return to Python per round)",
            "temps": [round(t, 4) for t in lad.temps], "swap_rates": [round(r, 3) for r in lad.swap_rates()],
-           "cold_phi": chains[lad.cold_local()].stats()["phi"]}
+           "mixing": lad.mixing(), "cold_phi": chains[lad.cold_local()].stats()["phi"]}
     lad.close()
     for c in chains:
         c.close()
@@ -405,7 +405,7 @@ def config4_ranks(tt, ds, ex, dist, coll_dev, rank, world, device, swap_every=10
            "proposals_per_s": round(world * swap_every * rounds / el, 1), "ms_per_round": round(el / rounds * 1e3, 4),
            "allgather_us_per_round": round(gat * 1e6, 2), "allgather_us_per_round_max_rank": round(gat_max * 1e6, 2),
            "temps": [round(x, 4) for x in lad.temps], "swap_rates": [round(r, 3) for r in lad.swap_rates()],
-           "collective": "allgather of 8 B per rank (%s)" % ("RCCL" if coll_dev == "cuda" else "gloo")}
+           "mixing": lad.mixing(), "collective": "allgather of 8 B per rank (%s)" % ("RCCL" if coll_dev == "cuda" else "gloo")}
     for c in chains:
         c.close()
     if rank == 0:  # the one-process ladder of the same replicas

@@ -145,6 +145,44 @@ class TemperingLadder:
             hasattr(c, "h") and getattr(c, "ctx", None) is self.chains[0].ctx and
             getattr(getattr(c, "params", None), "engine", None) == 0 for c in self.chains)
         self.rounds = None
+        # mixing statistics (_observe): a replica is labelled "up" after it visits level 0 and "down"
+        # after it visits the top level; a round trip is a 0 -> top -> 0 journey of one replica
+        self.label = np.zeros(self.R, dtype=np.int8)  # 0 none yet, 1 up, -1 down
+        self.label[0] = 1
+        if self.R > 1:
+            self.label[self.R - 1] = -1
+        self._went_up = self.label == 1  # visited level 0 before its current "down" label
+        self.trips = np.zeros(self.R, dtype=np.int64)  # completed round trips per replica
+        self.up_visits = np.zeros(self.R, dtype=np.int64)  # per level: rounds its replica was labelled up
+        self.lab_visits = np.zeros(self.R, dtype=np.int64)  # per level: rounds its replica had a label
+
+    def _observe(self, levels):
+        """Update the round-trip counts and the up-fraction histogram after a swap round
+        (levels[g] = the level of replica g)."""
+        if self.R < 2:
+            return
+        top = self.R - 1
+        for g in range(self.R):
+            lv = int(levels[g])
+            if lv == 0:
+                if self.label[g] == -1 and self._went_up[g]:
+                    self.trips[g] += 1
+                self.label[g] = 1
+                self._went_up[g] = True
+            elif lv == top:
+                self.label[g] = -1
+            if self.label[g] != 0:
+                self.lab_visits[lv] += 1
+                self.up_visits[lv] += self.label[g] == 1
+
+    def mixing(self):
+        """Round trips (0 -> top -> 0, all replicas), rounds per round trip, and per level
+        the fraction of labelled visits by replicas heading up (1 at T = 1 falling to 0 at
+        the top for a ladder whose replicas diffuse over all of it)."""
+        n = int(self.trips.sum())
+        return {"round_trips": n, "rounds_per_round_trip": round(self.rnd / n, 1) if n else None,
+                "up_fraction": [round(float(u) / v, 3) if v else None
+                                for u, v in zip(self.up_visits, self.lab_visits)]}
 
     def gid(self, j):
         return self.ex.rank * self.local + j
@@ -179,6 +217,7 @@ class TemperingLadder:
             if new[g] != self.levels[g] and not self.resident:  # (resident: posted with the next round)
                 ch.set_temperature(float(self.temps[new[g]]))
         self.levels = new
+        self._observe(new)
         self.rnd += 1
         return allphi
 
@@ -215,6 +254,7 @@ class TemperingLadder:
         for j in range(rounds):
             self._trace.update(phis[j].tobytes())
             self._trace.update(lv_out[j].tobytes())
+            self._observe(lv_out[j])
         self.tried += tried[:R - 1]
         self.accepted += acc[:R - 1]
         self.levels = levels

@@ -325,11 +325,12 @@ def test_library_tempering_loop_equals_round_by_round(tt, ds, ctx):
                 lad.step(10 if r < 25 else 4)
         lad.close()
         runs.append((lad.trace_digest(), list(lad.levels), list(lad.tried), list(lad.accepted),
-                     [c.model() for c in chains], [c.stats() for c in chains], lad.rnd))
+                     [c.model() for c in chains], [c.stats() for c in chains], lad.rnd, lad.mixing()))
         for c in chains:
             c.close()
     a, b = runs
     assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2] and a[3] == b[3] and a[6] == b[6] == 36
+    assert a[7] == b[7]  # round trips and up-fractions: the library loop observes every round's levels
     for ma, mb, x, y in zip(a[4], b[4], a[5], b[5]):
         assert same_models(ma, mb)
         assert x["phi"] == y["phi"] and x["accepted"] == y["accepted"] and x["proposed"] == y["proposed"]

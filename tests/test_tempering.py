@@ -196,3 +196,29 @@ def test_resident_rounds_not_under_a_gpu_collective():
     assert tempering.TemperingLadder(chains, exchange=tempering.Exchange(FakeDist(2), "cpu")).resident
     assert not tempering.TemperingLadder(chains, exchange=tempering.Exchange(FakeDist(2), "cuda:0")).resident
     assert not tempering.TemperingLadder(chains, resident=False).resident
+
+
+def test_round_trip_counting():
+    """mixing(): a replica's 0 -> top -> 0 journey is one round trip; the
+    up-fraction histogram labels a visit by the last extreme the replica saw."""
+    chains = [ToyChain(s) for s in range(3)]
+    lad = tempering.TemperingLadder(chains, tmax=4.0, seed=1)
+    # replica 0 climbs to the top and back, replica 2 goes down to 0 and back up (no trip yet)
+    seq = [[1, 0, 2], [2, 0, 1], [2, 1, 0], [1, 2, 0], [0, 2, 1]]
+    for lv in seq:
+        lad._observe(np.array(lv))
+        lad.rnd += 1
+    m = lad.mixing()
+    assert list(lad.trips) == [1, 0, 0] and m["round_trips"] == 1 and m["rounds_per_round_trip"] == 5.0
+    assert m["up_fraction"][0] == 1.0 and m["up_fraction"][2] == 0.0
+
+
+def test_cold_replica_ladder_makes_round_trips():
+    chains = [ToyChain(s) for s in range(4)]
+    lad = tempering.TemperingLadder(chains, tmax=16.0, seed=5)
+    for _ in range(3000):
+        lad.step(2)
+    m = lad.mixing()
+    assert m["round_trips"] > 10
+    f = [x for x in m["up_fraction"]]
+    assert f[0] == 1.0 and f[-1] == 0.0 and all(a >= b - 0.1 for a, b in zip(f, f[1:]))
