@@ -63,6 +63,14 @@ int tdt_chain_set_exact_every(td_chain *ch, int k);
  * idle watchdog can fire first (the race of a descheduled host thread).  The
  * command must then be re-issued to a new launch with the same results.  0 = off. */
 int tdt_set_server_post_delay(int ms);
+/* Resident tempering rounds (td_rounds_*): at the next launch the workgroups of
+ * the listed chains return at their first wait, before the host posts the
+ * round, while the others run it -- the race of a workgroup's idle watchdog
+ * firing just as a round is posted.  td_rounds_run must then re-post the round
+ * to a new launch in which the chains that ran it only report phi: every chain
+ * runs each round once, with the results of an undisturbed launch.  One-shot;
+ * ends the running launch. */
+int tdt_rounds_force_exit(td_rounds *r, const int32_t *slots, int64_t nslots);
 /* The block-wide exact sequential sum (exact_sum.h, used for chi^2 over long
  * ray lists): prefix[k] = C0 + term[0] + ... + term[k] added strictly left to
  * right in FP64 (MCsub.jl:170-172).  *fast = 1 when the parallel path proved

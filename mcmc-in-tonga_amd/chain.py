@@ -307,9 +307,26 @@ def run_chains(TD_parameters, dataStruct, chains, engine=_lib.TD_ENGINE_DEVICE, 
     (one workgroup per chain, concurrently, as the reference's workers run);
     chains whose stretches differ (resumed from different checkpoints) run in
     separate launches.  Each chain's model_hist is the one TD_inversion_function
-    returns for it alone."""
+    returns for it alone.
+
+    HOST and DROPIN chains call the context's td_evaluate per proposal: they
+    share its incremental shadow (one model at a time), so they run one chain
+    after another, as separate workers would, instead of interleaved stretches
+    that would rebuild the shadow at every switch."""
     chains = list(chains)
     seeds = seeds or [None] * len(chains)
+    if engine != _lib.TD_ENGINE_DEVICE:
+        out = []
+        for c, s in zip(chains, seeds):
+            d = _ChainDriver(TD_parameters, dataStruct, c, s, None, engine, checkpoint_dir, verbose, 1.0, None)
+            while True:
+                k = d.next_stretch()
+                if k is None:
+                    break
+                d.ch.run(k)
+                d.after_stretch()
+            out.append(d.finish())
+        return out
     drv = [_ChainDriver(TD_parameters, dataStruct, c, s, None, engine, checkpoint_dir, verbose, 1.0, None)
            for c, s in zip(chains, seeds)]
     live = list(drv)

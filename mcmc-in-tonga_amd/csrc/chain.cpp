@@ -19,6 +19,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -71,6 +72,7 @@ struct td_rounds {
     long long seq = 0;
     double tr_first = 0.0, tr_last = 0.0;  // diagnostic (TD_ROUNDS_TRACE): summed arrival times, rounds
     long long tr_n = 0;
+    std::vector<char> force_exit;  // testing (tdt_rounds_force_exit): one-shot, per chain
 };
 
 namespace {
@@ -484,19 +486,51 @@ int server_stop(td_chain *ch);
 // box) queues, so work on any other stream -- another context's, this
 // context's own, torch's, RCCL's -- may sit behind it until its watchdog.
 // servers_quiesce stops them before such work (include/tdstar.h, contexts).
-thread_local std::vector<td_chain *> t_servers;
-thread_local std::vector<td_rounds *> t_rounds;  // resident tempering launches of this thread
+// One registry for the process, each entry tagged with the thread that started
+// it: a thread quiesces its own launches, and a launch stopped or freed on any
+// thread (a Python finaliser may run anywhere) leaves no entry behind.
+struct Resident {
+    td_chain *srv;    // a td_evaluate shadow server, or
+    td_rounds *rnd;   // a resident tempering launch
+    std::thread::id owner;
+};
+std::mutex g_res_mu;
+std::vector<Resident> g_res;
 int rounds_stop(td_rounds *r);
+
+void servers_register(td_chain *ch) {
+    std::lock_guard<std::mutex> g(g_res_mu);
+    g_res.push_back(Resident{ch, nullptr, std::this_thread::get_id()});
+}
+void servers_unregister(td_chain *ch) {
+    std::lock_guard<std::mutex> g(g_res_mu);
+    g_res.erase(std::remove_if(g_res.begin(), g_res.end(), [&](const Resident &e) { return e.srv == ch; }),
+                g_res.end());
+}
+void rounds_register(td_rounds *r) {
+    std::lock_guard<std::mutex> g(g_res_mu);
+    g_res.push_back(Resident{nullptr, r, std::this_thread::get_id()});
+}
+void rounds_unregister(td_rounds *r) {
+    std::lock_guard<std::mutex> g(g_res_mu);
+    g_res.erase(std::remove_if(g_res.begin(), g_res.end(), [&](const Resident &e) { return e.rnd == r; }),
+                g_res.end());
+}
 
 }  // namespace
 
 namespace tdstar {
 void servers_quiesce(const td_chain *keep) {
-    const std::vector<td_chain *> run = t_servers;
-    for (td_chain *c : run)
-        if (c != keep) (void)server_stop(c);
-    const std::vector<td_rounds *> rr = t_rounds;
-    for (td_rounds *r : rr) (void)rounds_stop(r);
+    std::vector<Resident> mine;
+    {
+        std::lock_guard<std::mutex> g(g_res_mu);
+        for (const Resident &e : g_res)
+            if (e.owner == std::this_thread::get_id()) mine.push_back(e);
+    }
+    for (const Resident &e : mine) {
+        if (e.srv && e.srv != keep) (void)server_stop(e.srv);
+        if (e.rnd) (void)rounds_stop(e.rnd);
+    }
 }
 }  // namespace tdstar
 
@@ -541,7 +575,7 @@ int server_stop(td_chain *ch) {
     hipError_t e = hipStreamSynchronize(ch->srv_stream);  // the kernel returns (QUIT, or its idle watchdog)
     ch->srv_running = false;
     ch->srv_has_pending = false;  // the kernel undid it
-    t_servers.erase(std::remove(t_servers.begin(), t_servers.end(), ch), t_servers.end());
+    servers_unregister(ch);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "chain server exit");
     adopt_scalars(ch);
     return TD_OK;
@@ -568,7 +602,7 @@ int server_start(td_chain *ch) {
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (server)");
     ch->srv_running = true;
     ch->srv_last = std::chrono::steady_clock::now();
-    t_servers.push_back(ch);
+    servers_register(ch);
     return TD_OK;
 }
 
@@ -588,7 +622,7 @@ int server_post(td_chain *ch) {
             const hipError_t e = hipStreamSynchronize(ch->srv_stream);
             ch->srv_running = false;
             ch->srv_has_pending = false;
-            t_servers.erase(std::remove(t_servers.begin(), t_servers.end(), ch), t_servers.end());
+            servers_unregister(ch);
             if (e != hipSuccess) return hip_err(ch->ctx, e, "chain server exit");
             adopt_scalars(ch);
             return kExitedEarly;
@@ -611,7 +645,7 @@ int rounds_stop(td_rounds *r) {
     *vol(&b->seq) = ++r->seq;
     const hipError_t e = hipStreamSynchronize(r->stream);  // every workgroup returns (QUIT or its watchdog)
     r->running = false;
-    t_rounds.erase(std::remove(t_rounds.begin(), t_rounds.end(), r), t_rounds.end());
+    rounds_unregister(r);
     if (e != hipSuccess) return hip_err(r->ctx, e, "tempering rounds exit");
     for (td_chain *ch : r->chains) adopt_scalars(ch);
     return TD_OK;
@@ -639,7 +673,7 @@ int rounds_start(td_rounds *r) {
     e = chain_run(r->desc_host, r->desc_dev, nc, LLONG_MAX, r->stream, &sa);
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (tempering rounds)");
     r->running = true;
-    t_rounds.push_back(r);
+    rounds_register(r);
     return TD_OK;
 }
 
@@ -691,10 +725,24 @@ int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out)
     for (int k = 0; k < nc; ++k)
         if (!(temps[k] > 0.0)) return set_err(r->ctx, TD_ERR_ARG, "td_rounds_run: need T > 0");
     TD_HIP(r->ctx, hipSetDevice(r->ctx->device));
+    // ran[k]: chain k ran this round in a launch that was lost (another workgroup's idle watchdog
+    // fired as the round was posted); the retry asks it only to report phi again (RoundSlot::skip)
+    std::vector<char> ran((size_t)nc, 0);
+    RoundBox *b = r->rb_host;
     for (int attempt = 0;; ++attempt) {
+        const bool forcing = !r->force_exit.empty();  // testing: tdt_rounds_force_exit
+        for (int k = 0; k < nc; ++k) b->slot[k].idle = (forcing && r->force_exit[(size_t)k]) ? 1 : 0;
         int rc = rounds_start(r);
         if (rc) return rc;
-        RoundBox *b = r->rb_host;
+        if (forcing) {  // the forced workgroups return at their first wait, before the round is posted
+            const auto tf = std::chrono::steady_clock::now();
+            for (int k = 0; k < nc; ++k)
+                while (r->force_exit[(size_t)k] && !*vol(&b->slot[k].exited))
+                    if (std::chrono::steady_clock::now() - tf > std::chrono::seconds(20))
+                        return set_err(r->ctx, TD_ERR_HIP, "tempering rounds: forced exit never came");
+            r->force_exit.clear();
+            for (int k = 0; k < nc; ++k) b->slot[k].idle = 0;
+        }
         for (int k = 0; k < nc; ++k) {  // the chain's temperature: its host params too (td_chain_set_temperature)
             td_chain *ch = r->chains[(size_t)k];
             ch->prm.temperature = temps[k];
@@ -703,6 +751,7 @@ int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out)
             ch->dev.params = ch->P;
             b->slot[k].T = ch->P.temperature;
             b->slot[k].inv_2t = ch->P.inv_2t;
+            b->slot[k].skip = ran[(size_t)k];
         }
         b->cmd = kRoundRun;
         b->K = (int)K;
@@ -748,16 +797,24 @@ int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out)
                     return set_err(r->ctx, TD_ERR_HIP, "tempering rounds: no answer in 60 s");
             }
         if (!lost) break;
-        // the launch returned between rounds (state consistent, nothing of this round run):
-        // collect it and post the round again to a new launch
+        // Some workgroup returned at the round boundary before it saw this round (its idle
+        // watchdog), while others may have run it.  End the launch (QUIT for the ones still
+        // waiting; every state is consistent between rounds), note who ran the round, and post it
+        // again to a new launch: the chains that ran it only report phi (skip).
+        b->cmd = kRoundQuit;
+        b->K = 0;
+        std::atomic_thread_fence(std::memory_order_release);
+        *vol(&b->seq) = ++r->seq;
         const hipError_t e = hipStreamSynchronize(r->stream);
         r->running = false;
-        t_rounds.erase(std::remove(t_rounds.begin(), t_rounds.end(), r), t_rounds.end());
+        rounds_unregister(r);
         if (e != hipSuccess) return hip_err(r->ctx, e, "tempering rounds exit");
         for (td_chain *ch : r->chains) adopt_scalars(ch);
-        --r->seq;  // this seq was never run
+        for (int k = 0; k < nc; ++k)
+            if (*vol(&b->slot[k].done) == sq) ran[(size_t)k] = 1;
         if (attempt > 2) return set_err(r->ctx, TD_ERR_HIP, "tempering rounds: the launch keeps returning");
     }
+    for (int k = 0; k < nc; ++k) b->slot[k].skip = 0;
     std::atomic_thread_fence(std::memory_order_acquire);
     for (int k = 0; k < nc; ++k) {
         td_chain *ch = r->chains[(size_t)k];
@@ -817,11 +874,16 @@ int td_rounds_temper(td_rounds *r, int64_t M, int64_t K, const double *temps, in
     const int64_t R = (int64_t)r->chains.size();
     std::vector<double> T((size_t)R), phi((size_t)R);
     std::vector<int64_t> nl((size_t)R);
-    for (int64_t j = 0; j < M; ++j) {
+    {  // levels must be a permutation of 0..R-1 before any round runs (td_swap_decide keeps it one)
+        std::vector<char> seen((size_t)R, 0);
         for (int64_t k = 0; k < R; ++k) {
-            if (levels[k] < 0 || levels[k] >= R) return set_err(r->ctx, TD_ERR_ARG, "td_rounds_temper: levels");
-            T[(size_t)k] = temps[levels[k]];
+            if (levels[k] < 0 || levels[k] >= R || seen[(size_t)levels[k]])
+                return set_err(r->ctx, TD_ERR_ARG, "td_rounds_temper: levels are not a permutation");
+            seen[(size_t)levels[k]] = 1;
         }
+    }
+    for (int64_t j = 0; j < M; ++j) {
+        for (int64_t k = 0; k < R; ++k) T[(size_t)k] = temps[levels[k]];
         const int rc = td_rounds_run(r, K, T.data(), phi.data());
         if (rc) return rc;
         if (td_swap_decide(R, phi.data(), levels, temps, rnd0 + j, seed, nl.data(), tried, accepted))
@@ -1281,6 +1343,20 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
     const double v[8] = {(double)p.action, (double)p.active, (double)p.valid, (double)p.index, p.x, p.y, p.z, p.zeta};
     std::memcpy(out, v, sizeof v);
     return 0;
+}
+int tdt_rounds_force_exit(td_rounds *r, const int32_t *slots, int64_t nslots) {
+    if (!r || nslots < 0 || (nslots > 0 && !slots)) return TD_ERR_ARG;
+    const int nc = (int)r->chains.size();
+    std::vector<char> f((size_t)nc, 0);
+    for (int64_t i = 0; i < nslots; ++i) {
+        if (slots[i] < 0 || slots[i] >= nc) return TD_ERR_ARG;
+        f[(size_t)slots[i]] = 1;
+    }
+    // takes effect at the next launch: end the running one (states are consistent between rounds)
+    const int rc = rounds_stop(r);
+    if (rc) return rc;
+    r->force_exit = nslots > 0 ? f : std::vector<char>();
+    return TD_OK;
 }
 int tdt_set_server_post_delay(int ms) {
     if (ms < 0) return TD_ERR_ARG;

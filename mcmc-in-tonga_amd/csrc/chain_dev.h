@@ -158,7 +158,11 @@ struct RoundSlot {
     long long done;    // device -> host: seq of the last round finished
     double phi;        // the chain's phi after that round
     long long exited;  // the workgroup returned (QUIT, or its idle watchdog at a round boundary)
-    long long pad[3];
+    // host -> device: 1 = this chain already ran the posted round in a launch that was lost
+    // (some other workgroup's watchdog fired as the round was posted): report phi again, run nothing
+    long long skip;
+    long long idle;  // testing (tdt_rounds_force_exit): > 0 = the idle watchdog of the launch's first wait, ticks
+    long long pad;
 };
 struct RoundBox {
     long long seq;  // host -> device (written last)

@@ -233,7 +233,7 @@ struct Shared {
     // resident tempering rounds: the temperature of the current round (for reject_bound) and its last seq
     double rT, rinv2t;
     long long rseq;
-    int rK;
+    int rK, rskip;
     long long srv_seq, srv_busy_c, srv_busy_w;
     long long mbox[32];  // server mode: the last command read from the mailbox
     OrphanRec orph[kOrphanLds];
@@ -716,6 +716,10 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
 // command: RUN (K proposals at the slot's new temperature) or QUIT; silence
 // past the idle watchdog is a QUIT (the state is consistent between rounds).
 // Results in sh.rK / sh.rT / sh.rinv2t / sh.srv_quit.
+// A RUN posted with the slot's `skip` set (the chain ran that round in a launch
+// the host lost, chain.cpp td_rounds_run) is answered with phi at once and
+// waited past: the chain runs each round exactly once.  `phi` = the chain's
+// exact phi (the launch's first wait: its stored one).
 __device__ void round_wait(RoundBox *rb, int b, Shared &sh, int lane, bool publish, double phi) {
     RoundSlot *slot = &rb->slot[b];
     // The mailbox is coherent pinned host memory and every access to it is a system-scope atomic,
@@ -727,20 +731,32 @@ __device__ void round_wait(RoundBox *rb, int b, Shared &sh, int lane, bool publi
         __builtin_amdgcn_s_waitcnt(0);
         mb_store(&slot->done, sh.rseq);
     }
-    const long long seen = sh.rseq;
+    long long seen = sh.rseq;
+    long long idle = kServerIdleTicks;
+    if (!publish) {  // a launch's first wait: the testing override of the watchdog
+        const long long o = mb_load(&slot->idle);
+        if (o > 0) idle = o;
+    }
     long long t0 = (long long)wall_clock64();
     while (true) {
         const long long sq = mb_load(&rb->seq);
         if (sq != seen) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (lane == 0) {
-                // (the host wrote them before seq: three loads in flight together)
+                // (the host wrote them before seq: four loads in flight together)
                 const long long w = mb_load(reinterpret_cast<const long long *>(rb) + 1);  // cmd | K << 32
                 const long long tb = mb_load(reinterpret_cast<const long long *>(&slot->T));
                 const long long ib = mb_load(reinterpret_cast<const long long *>(&slot->inv_2t));
+                const long long sk = mb_load(&slot->skip);
                 const int cmd = (int)(w & 0xffffffffll), K = (int)(w >> 32);
                 sh.rseq = sq;
-                if (cmd == kRoundRun && K > 0) {
+                sh.rskip = 0;
+                if (cmd == kRoundRun && K > 0 && sk) {  // ran already: report it again
+                    mb_store(reinterpret_cast<long long *>(&slot->phi), __double_as_longlong(phi));
+                    __builtin_amdgcn_s_waitcnt(0);
+                    mb_store(&slot->done, sq);
+                    sh.rskip = 1;
+                } else if (cmd == kRoundRun && K > 0) {
                     sh.rK = K;
                     sh.rT = __longlong_as_double(tb);
                     sh.rinv2t = __longlong_as_double(ib);
@@ -750,9 +766,14 @@ __device__ void round_wait(RoundBox *rb, int b, Shared &sh, int lane, bool publi
                 }
             }
             wave_sync_lds();
+            if (sh.rskip) {
+                seen = sq;
+                t0 = (long long)wall_clock64();
+                continue;
+            }
             return;
         }
-        if ((long long)wall_clock64() - t0 > kServerIdleTicks) {
+        if ((long long)wall_clock64() - t0 > idle) {
             if (lane == 0) sh.srv_quit = 1;
             wave_sync_lds();
             return;
@@ -1028,7 +1049,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         if (rbx) {  // the first round (the last one done is in the slot)
             if (lane == 0) sh.rseq = mb_load(&rbx->slot[bchain].done);
             wave_sync_lds();
-            round_wait(rbx, bchain, sh, lane, false, 0.0);
+            round_wait(rbx, bchain, sh, lane, false, sh.phi);  // (the stored phi is exact)
         }
         if (lane == 0 && iters > 0 && !((mb || rbx) && sh.srv_quit)) {
             if (nscript) {

@@ -262,10 +262,14 @@ class TemperingLadder:
         return phis[-1].copy()
 
     def close(self):
-        """End the resident launch (the chains' counts and models are current after it)."""
+        """End the resident launch (the chains' counts and models are current after it).
+        A resident round runs at the temperatures posted with it, so the last swap's
+        levels reach the chains only here: each chain leaves at its ladder level's T."""
         if self.rounds is not None:
             self.rounds.close()
             self.rounds = None
+            for j, ch in enumerate(self.chains):
+                ch.set_temperature(float(self.temps[self.levels[self.gid(j)]]))
 
     def trace_digest(self):
         """sha256 of every round's gathered phis and new levels so far."""

@@ -16,6 +16,11 @@ MCsub.jl:123-185) and against from-scratch evaluates of the chain's model.
   proposals, DEVICE == HOST, final state == full evaluate;
 * the drop-in leg: the DROPIN engine (public td_evaluate per proposal, its
   resident incremental path) == HOST over bench's 1550 proposals.
+
+The end states are also checked against the C oracle (oracle/tstar_oracle.c,
+a scalar restatement of MCsub.jl:123-185), not only against another HIP path:
+the 125k-proposal config-3 chain, 4 of the 256 batch chains, and a stress
+chain on a 1500-ray subset of the config-5 rays at 3000 cells.
 """
 import numpy as np
 import pytest
@@ -38,6 +43,17 @@ def state_is_full_evaluate(ctx, ch):
     return m
 
 
+def state_is_oracle(orc, ds, ch):
+    """The chain's final (ptS, phi) == the C oracle's evaluate of its model, bit for bit
+    (the oracle is the checker here, never the thing measured)."""
+    m = ch.model()
+    ref = orc.evaluate(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig, m.cells())
+    assert ref["rc"] == 0
+    assert ref["phi"] == m.phi == ch.stats()["phi"]
+    assert np.array_equal(ref["ptS"], m.ptS)
+    return m
+
+
 def agree(a, b):
     sa, sb = a.stats(), b.stats()
     assert sa["phi"] == sb["phi"], (sa, sb)
@@ -55,7 +71,7 @@ def ctx(tt, ds):
 
 
 @pytest.mark.timeout(600)
-def test_config3_headline_run_follows_host(tt, ds, ctx):
+def test_config3_headline_run_follows_host(tt, ds, ctx, orc):
     prm = tt.define_TDstructrure().replace(max_cells=2 * 5000)
     model = tt.random_model(5000, 3)
     dev = tt.Chain(ctx, tt.chain_params(prm, ds, seed=1000, chain=1), model)
@@ -70,12 +86,13 @@ def test_config3_headline_run_follows_host(tt, ds, ctx):
             assert same_models(m, host.model())
     assert st["iterations"] == launches * BENCH_ITERS
     assert sum(st["accepted"]) > 10000 and min(st["accepted"]) > 0  # every action was accepted many times
+    state_is_oracle(orc, ds, dev)
     dev.close()
     host.close()
 
 
 @pytest.mark.timeout(600)
-def test_many_chains_batch_follows_solo_and_host(tt, ds, ctx):
+def test_many_chains_batch_follows_solo_and_host(tt, ds, ctx, orc):
     prm = tt.define_TDstructrure().replace(max_cells=2 * 5000)
     model = tt.random_model(5000, 3)
     C = 256
@@ -94,6 +111,7 @@ def test_many_chains_batch_follows_solo_and_host(tt, ds, ctx):
         agree(chains[j], host)
         m = state_is_full_evaluate(ctx, chains[j])
         assert same_models(m, solo.model()) and same_models(m, host.model())
+        state_is_oracle(orc, ds, chains[j])
         solo.close()
         host.close()
     for c in chains:
@@ -169,3 +187,29 @@ def test_dropin_leg_follows_host(tt, ds):
     host.close()
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.timeout(600)
+def test_stress_subset_chain_matches_oracle(tt, orc):
+    """Config 5's rays, first 1500 (the HBM layout: tiles, rays and order out of
+    LDS), 3000 cells, 1500 proposals: DEVICE == HOST, and the final state ==
+    the C oracle's evaluate of the final model."""
+    full = tt.synthetic_rays(10000, seed=5)
+    ds = tt.sub_datastruct(full, 0, 1500)
+    c = tt.TdContext.from_datastruct(ds)
+    c.set_incremental(c.INCR_FULL)
+    prm = tt.define_TDstructrure().replace(max_cells=4500)
+    model = tt.random_model(3000, 5)
+    dev = tt.Chain(c, tt.chain_params(prm, ds, seed=78, chain=1), model)
+    assert tt.lib().tdt_chain_set_lds_mode(dev.h, 1) == 0
+    host = tt.Chain(c, tt.chain_params(prm, ds, seed=78, chain=1, engine=tt.TD_ENGINE_HOST), model)
+    for k in (300, 1200):
+        dev.run(k)
+        host.run(k)
+        st = agree(dev, host)
+    assert sum(st["accepted"]) > 100
+    m = state_is_oracle(orc, ds, dev)
+    assert same_models(m, host.model())
+    dev.close()
+    host.close()
+    c.close()

@@ -305,6 +305,41 @@ def test_resident_rounds_equal_launch_per_round(tt, ds, ctx):
         assert x["iterations"] == y["iterations"] == 20 * 10 + 10 * 7
 
 
+def test_resident_rounds_partial_exit(tt, ds, ctx):
+    """The watchdog race: some workgroups of the resident launch
+    return at a round boundary just as the host posts the next round, while
+    the others run it (tdt_rounds_force_exit makes that happen on purpose).
+    td_rounds_run must post the round again so that every chain runs it once:
+    the ladder equals one launch per round, iteration counts included.  After
+    close() every chain sits at its ladder level's temperature: more
+    proposals on the chains alone still agree."""
+    prm = tt.define_TDstructrure().replace(max_cells=600)
+    runs = []
+    for resident in (True, False):
+        chains = [make(tt, ctx, prm, tt.random_model(200 + 30 * j, 160 + j), 160 + j, tt.TD_ENGINE_DEVICE,
+                       chain=1 + j) for j in range(5)]
+        lad = tt.TemperingLadder(chains, tmax=8.0, seed=5, resident=resident)
+        trace = []
+        for r in range(24):
+            if resident and r in (1, 7, 8, 15):
+                forced = {1: [0], 7: [1, 3], 8: [4], 15: [0, 2, 3]}[r]
+                arr = (ctypes.c_int32 * len(forced))(*forced)
+                assert tt.lib().tdt_rounds_force_exit(lad.rounds.h, arr, len(forced)) == 0
+            trace.append([list(lad.step(10)), list(lad.levels)])
+        lad.close()
+        for c in chains:  # alone, after the ladder: each at the temperature of its final level
+            c.run(60)
+        runs.append((trace, [c.model() for c in chains], [c.stats() for c in chains], lad.trace_digest()))
+        for c in chains:
+            c.close()
+    (ta, ma, sa, da), (tb, mb, sb, db) = runs
+    assert ta == tb and da == db
+    for a, b, x, y in zip(ma, mb, sa, sb):
+        assert same_models(a, b)
+        assert x["phi"] == y["phi"] and x["accepted"] == y["accepted"] and x["proposed"] == y["proposed"]
+        assert x["iterations"] == y["iterations"] == 24 * 10 + 60
+
+
 def test_library_tempering_loop_equals_round_by_round(tt, ds, ctx):
     """TemperingLadder.run (td_rounds_temper: the resident launch with the swap
     steps decided in the library between rounds, no return to Python per
