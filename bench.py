@@ -293,8 +293,7 @@ def main():
         out["tempering"] = {"replicas": ladder.R, "temps": [round(t, 4) for t in ladder.temps],
                             "swap_rates": [round(r, 3) for r in ladder.swap_rates()]}
     if dist is not None and a.config4:  # every rank: config 4, one tempered replica per rank, RCCL allgather
-        c4 = config4_ranks(tt, ds, tt.Exchange(dist, coll_dev), dist, coll_dev, rank, world, local,
-                           rounds=a.config4_rounds)
+        c4 = config4_ranks(tt, ds, dist, coll_dev, rank, world, local, rounds=a.config4_rounds)
         if rank == 0:
             out["config4_ranks"] = c4
     if dist is not None and not a.no_stress:  # every rank: config 5, one stress chain per rank
@@ -313,6 +312,7 @@ def main():
         out["stress"] = stress(tt, a.stress_iters)
     if rank == 0 and a.config4:
         out["config4_tempering"] = tempering_config4(tt, ctx, ds, rounds=a.config4_rounds)
+        out["exchange_cost"] = exchange_cost(tt, ctx, ds, rounds=a.config4_rounds)
     if rank == 0 and not a.no_full_evaluate:  # SURVEY 8f rows 2 and 4, measured beside their CPU restatements
         out["posterior_maps"] = posterior_maps(tt, ctx, ds)
         out["ingest_trilinear"] = ingest_trilinear(tt)
@@ -337,30 +337,82 @@ def main():
         dist.destroy_process_group()
 
 
+def ladder_modes(tt, device):
+    """The three ways one process runs a resident ladder: the swaps decided by
+    the host between posted rounds (td_rounds_temper), decided inside the
+    kernel with the phis meeting in device memory (td_rounds_exchange, no
+    collective), and decided inside the kernel after an RCCL allgather of the
+    library's own one-rank communicator (the exchange stream waiting on the
+    kernel's flag: the mechanism a rank uses at N GPUs)."""
+    return [("host_decided", False, None), ("device_swaps", True, None),
+            ("device_swaps_rccl", True, tt.NativeComm(device))]
+
+
+def run_ladder(tt, chains, device_swaps, comm, swap_every, rounds, warm=20):
+    ex = tt.Exchange()
+    ex.comm = comm
+    lad = tt.TemperingLadder(chains, ex, tmax=8.0, seed=4242, device_swaps=device_swaps)
+    lad.run(warm, swap_every)
+    t0 = time.perf_counter()
+    lad.run(rounds, swap_every)  # one resident launch: the swap steps in the library or in the kernel
+    el = time.perf_counter() - t0
+    lad.close()
+    out = {"ms_per_round": round(el / rounds * 1e3, 4),
+           "proposals_per_s": round(len(chains) * swap_every * rounds / el, 1),
+           "trace_sha256": lad.trace_digest()}
+    if lad.timing:
+        out["split_us_per_round"] = {k: lad.timing[k] for k in ("exchange_us_per_round", "proposals_us_per_round",
+                                                                 "slowest_replica_wait_us_per_round")}
+    return out, lad
+
+
 def tempering_config4(tt, ctx, ds, nrep=8, ncells=2000, swap_every=10, rounds=300):
     """BASELINE config 4's ladder on ONE GPU: 8 tempered replicas x 2000 cells
     (seeds 100 + replica), geometric T in [1, 8], a swap round every 10
-    proposals; the replicas run in one td_chain_run_batch launch per round, the
-    allgather is the identity in one process (the N-GPU runs put one rank per
-    GPU and gather over RCCL: tests/test_gpu_config4.py checks the two agree)."""
-    chains = config4_replicas(tt, ctx, ds, 0, nrep, ncells)
-    lad = tt.TemperingLadder(chains, tmax=8.0, seed=4242)
-    lad.run(20, swap_every)
-    ctx.timing(enable=True, reset=True)
-    t0 = time.perf_counter()
-    lad.run(rounds, swap_every)  # the resident launch, the swap steps in the library (td_rounds_temper)
-    el = time.perf_counter() - t0
-    ctx.timing(enable=False)
-    res = {"replicas": nrep, "cells": ncells, "swap_every": swap_every, "rounds": rounds,
-           "proposals_per_s": round(nrep * swap_every * rounds / el, 1),
-           "ms_per_round": round(el / rounds * 1e3, 4),
-           "rounds_by": "one resident k_chain_run launch; swap steps in the library between rounds "
-                        "(td_rounds_temper, no return to Python per round)",
-           "temps": [round(t, 4) for t in lad.temps], "swap_rates": [round(r, 3) for r in lad.swap_rates()],
-           "mixing": lad.mixing(), "cold_phi": chains[lad.cold_local()].stats()["phi"]}
-    lad.close()
-    for c in chains:
-        c.close()
+    proposals, one resident launch -- in each of ladder_modes' three ways,
+    which must leave the same trace (the top-level numbers: host_decided).
+    The N-GPU runs put one rank per GPU (config4_ranks)."""
+    res = {"replicas": nrep, "cells": ncells, "swap_every": swap_every, "rounds": rounds, "modes": {}}
+    digests = set()
+    for name, dev_swaps, comm in ladder_modes(tt, ctx.device):
+        chains = config4_replicas(tt, ctx, ds, 0, nrep, ncells)
+        out, lad = run_ladder(tt, chains, dev_swaps, comm, swap_every, rounds)
+        digests.add(out["trace_sha256"])
+        res["modes"][name] = out
+        if name == "host_decided":
+            res.update({"proposals_per_s": out["proposals_per_s"], "ms_per_round": out["ms_per_round"],
+                        "rounds_by": "one resident k_chain_run launch; swap steps in the library between rounds "
+                                     "(td_rounds_temper, no return to Python per round)",
+                        "temps": [round(t, 4) for t in lad.temps],
+                        "swap_rates": [round(r, 3) for r in lad.swap_rates()],
+                        "mixing": lad.mixing(), "cold_phi": chains[lad.cold_local()].stats()["phi"]})
+        for c in chains:
+            c.close()
+        if comm is not None:
+            comm.close()
+    res["modes_same_trace"] = len(digests) == 1
+    return res
+
+
+def exchange_cost(tt, ctx, ds, swap_every=10, rounds=300, ncells=2000):
+    """What the exchange step costs a rank of config 4 at N GPUs, measured on
+    one: ONE replica (replica 0), a round of 10 proposals, in ladder_modes'
+    three ways.  host_decided is the resident round with a host handshake;
+    device_swaps_rccl adds the real collective machinery (flag -> stream wait
+    -> ncclAllGather -> stream write -> kernel) that every round of a rank
+    pays, minus only the xGMI hop of a multi-GPU allgather."""
+    res = {"replicas": 1, "cells": ncells, "swap_every": swap_every, "rounds": rounds}
+    for name, dev_swaps, comm in ladder_modes(tt, ctx.device):
+        chains = config4_replicas(tt, ctx, ds, 0, 1, ncells)
+        out, _ = run_ladder(tt, chains, dev_swaps, comm, swap_every, rounds)
+        out.pop("trace_sha256")
+        res[name] = out
+        for c in chains:
+            c.close()
+        if comm is not None:
+            comm.close()
+    base = res["host_decided"]["ms_per_round"]
+    res["rccl_round_over_resident_round"] = round(res["device_swaps_rccl"]["ms_per_round"] / base, 4)
     return res
 
 
@@ -373,48 +425,95 @@ def config4_replicas(tt, ctx, ds, first, count, ncells=2000):
             for g in range(first, first + count)]
 
 
-def config4_ranks(tt, ds, ex, dist, coll_dev, rank, world, device, swap_every=10, rounds=300, warm=20):
+def config4_ranks(tt, ds, dist, coll_dev, rank, world, device, swap_every=10, rounds=300, warm=20):
     """BASELINE config 4 across the ranks: one tempered replica per rank
     (replica g = rank), geometric T in [1, 8] over the world, a swap round
-    every 10 proposals: the replica's launch, the allgather of every rank's
-    phi (torch.distributed: RCCL over xGMI with one rank per GPU) and the
-    same swap decision on every rank.  value = all ranks' proposals / the
-    max-over-ranks time.  Rank 0 then replays the same ladder in ONE process
-    (all `world` replicas on its GPU, identity gather): the swap traces'
-    digests must be equal."""
+    every 10 proposals.  Two ways, each timed over the same rounds, value =
+    all ranks' proposals / the max-over-ranks time:
+
+    * device_swaps (RCCL only): ONE resident launch per rank for all rounds;
+      each round the kernel raises a flag, the library's exchange stream
+      (waiting on it) runs ncclAllGather of every rank's phi over xGMI and
+      writes the round's done word, and the kernel decides the swaps itself
+      (td_rounds_exchange) -- no host in the loop;
+    * host_loop: TemperingLadder.step -- the resident round posted by the host,
+      Exchange.allgather through torch.distributed (RCCL, or gloo in the
+      one-GPU rehearsal), the decision in Python.
+
+    Rank 0 then replays the same ladder in ONE process (all `world` replicas
+    on its GPU): the swap traces' digests must be equal.  Each mode carries a
+    roofline block for the replica's kernel (latency-bound; the in-kernel byte
+    count over the timed region against HBM) and its per-round split."""
     import torch
 
     ctx = tt.TdContext.from_datastruct(ds, device=device)
-    chains = config4_replicas(tt, ctx, ds, rank, 1)
-    lad = tt.TemperingLadder(chains, ex, tmax=8.0, seed=4242)
-    for _ in range(warm):
-        lad.step(swap_every)
-    g0 = lad.gather_s
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(rounds):
-        lad.step(swap_every)
-    el = time.perf_counter() - t0
-    gat = (lad.gather_s - g0) / rounds
-    t = torch.tensor([el, gat], dtype=torch.float64, device=coll_dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el, gat_max = float(t[0].item()), float(t[1].item())
-    digest = lad.trace_digest()
     res = {"replicas": world, "ranks": world, "cells": 2000, "swap_every": swap_every, "rounds": rounds,
-           "proposals_per_s": round(world * swap_every * rounds / el, 1), "ms_per_round": round(el / rounds * 1e3, 4),
-           "allgather_us_per_round": round(gat * 1e6, 2), "allgather_us_per_round_max_rank": round(gat_max * 1e6, 2),
-           "temps": [round(x, 4) for x in lad.temps], "swap_rates": [round(r, 3) for r in lad.swap_rates()],
-           "mixing": lad.mixing(), "collective": "allgather of 8 B per rank (%s)" % ("RCCL" if coll_dev == "cuda" else "gloo")}
-    for c in chains:
-        c.close()
+           "collective": "allgather of 8 B per rank (%s)" % ("RCCL" if coll_dev == "cuda" else "gloo"), "modes": {}}
+    modes = (["device_swaps"] if coll_dev == "cuda" else []) + ["host_loop"]
+    digest = None
+    for mode in modes:
+        chains = config4_replicas(tt, ctx, ds, rank, 1)
+        if mode == "device_swaps":
+            ex = tt.Exchange(dist, coll_dev, native=device)
+            lad = tt.TemperingLadder(chains, ex, tmax=8.0, seed=4242, device_swaps=True)
+            lad.run(warm, swap_every)
+        else:
+            ex = tt.Exchange(dist, coll_dev)
+            lad = tt.TemperingLadder(chains, ex, tmax=8.0, seed=4242)
+            for _ in range(warm):
+                lad.step(swap_every)
+        b0 = chains[0].stats()["bytes"]
+        c0, g0, d0 = lad.compute_s, lad.gather_s, lad.decide_s
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        if mode == "device_swaps":
+            lad.run(rounds, swap_every)
+        else:
+            for _ in range(rounds):
+                lad.step(swap_every)
+        el = time.perf_counter() - t0
+        lad.close()
+        nbytes = chains[0].stats()["bytes"] - b0
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t[0].item())
+        out = {"proposals_per_s": round(world * swap_every * rounds / el_max, 1),
+               "ms_per_round": round(el_max / rounds * 1e3, 4), "trace_sha256": lad.trace_digest()}
+        if mode == "device_swaps":
+            tm = lad.timing
+            out["split_us_per_round"] = {"exchange": tm["exchange_us_per_round"],
+                                         "proposals": tm["proposals_us_per_round"],
+                                         "launch_amortized": round((tm["call_s"] - tm["kernel_span_s"]) / rounds * 1e6,
+                                                                   3)}
+        else:
+            out["split_us_per_round"] = {"compute": round((lad.compute_s - c0) / rounds * 1e6, 3),
+                                         "gather": round((lad.gather_s - g0) / rounds * 1e6, 3),
+                                         "decide": round((lad.decide_s - d0) / rounds * 1e6, 3)}
+        out["roofline"] = chain_roofline("k_chain_run (config-4 replica, resident rounds)",
+                                         model_bytes(int(ctx.P), int(ctx.n), 2000), swap_every * rounds, el, nbytes,
+                                         None, False)
+        out["roofline"]["latency"] = phase_cycles(tt, chains[0], 2000)
+        if digest is None:
+            digest = out["trace_sha256"]
+            res.update({"temps": [round(x, 4) for x in lad.temps], "swap_rates": [round(r, 3) for r in lad.swap_rates()],
+                        "mixing": lad.mixing()})
+        res["modes"][mode] = out
+        for c in chains:
+            c.close()
+        if ex.comm is not None:
+            ex.comm.close()
+    best = min(res["modes"].values(), key=lambda m: m["ms_per_round"])
+    res["proposals_per_s"], res["ms_per_round"] = best["proposals_per_s"], best["ms_per_round"]
+    res["roofline"] = best["roofline"]
     if rank == 0:  # the one-process ladder of the same replicas
         ref = config4_replicas(tt, ctx, ds, 0, world)
         lad1 = tt.TemperingLadder(ref, tmax=8.0, seed=4242)
-        for _ in range(warm + rounds):
-            lad1.step(swap_every)
+        lad1.run(warm + rounds, swap_every)
+        lad1.close()
         res["trace_sha256"] = digest
-        res["trace_matches_single_process"] = lad1.trace_digest() == digest
+        res["trace_matches_single_process"] = all(m["trace_sha256"] == lad1.trace_digest()
+                                                  for m in res["modes"].values())
         for c in ref:
             c.close()
     ctx.close()
@@ -432,17 +531,25 @@ def stress_chains(tt, dist, coll_dev, rank, world, device, iters):
     prm = tt.define_TDstructrure().replace(max_cells=40000)
     ch = tt.Chain(ctx, tt.chain_params(prm, ds, seed=77 + rank, chain=1 + rank), tt.random_model(20000, 5))
     ch.run(200)
+    b0 = ch.stats()["bytes"]
     torch.cuda.synchronize()
     dist.barrier()
+    ctx.timing(enable=True, reset=True)
     t0 = time.perf_counter()
     ch.run(iters)
     el = time.perf_counter() - t0
+    launches, kms = ctx.timing(kernel="chain_run")
+    ctx.timing(enable=False)
+    nbytes = ch.stats()["bytes"] - b0
     t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     res = {"chains": world, "rays": int(ctx.n), "cells": 20000, "iters_per_chain": iters,
            "proposals_per_s": round(world * iters / el, 1), "per_chain_proposals_per_s": round(iters / el, 1),
-           "phi_rank0": ch.stats()["phi"]}
+           "phi_rank0": ch.stats()["phi"],
+           "roofline": chain_roofline("k_chain_run<false, false> (rays in HBM), this rank's chain",
+                                      model_bytes(int(ctx.P), int(ctx.n), 20000), iters,
+                                      kms / 1e3 / max(launches, 1), nbytes, "k_chain_run/stress", iters == 2000)}
     ch.close()
     ctx.close()
     return res
@@ -497,15 +604,29 @@ def dropin(tt, ds, model, iters=1500, host_iters=300):
         ch.run(50)
         e0 = ch.stats()["evaluations"]
         ctx.timing(enable=True, reset=True)
+        dt = np.zeros(12, dtype=np.int64)
+        tt.lib().tdt_dropin_timing(ctx.h, 1, dt.ctypes.data_as(tt._lib._pi64))
         t0 = time.perf_counter()
         ch.run(k)
         el = time.perf_counter() - t0
+        tt.lib().tdt_dropin_timing(ctx.h, 1, dt.ctypes.data_as(tt._lib._pi64))
         ne = ch.stats()["evaluations"] - e0
         res = {"proposals_per_s": round(k / el, 1), "us_per_proposal": round(el / k * 1e6, 2), "evaluates": ne,
                "proposals": k}
         if engine == tt.TD_ENGINE_DROPIN:
             res["served_by"] = ("one resident k_chain_run per shadow chain, fed each td_evaluate / td_interpolate "
                                 "through a pinned mailbox (no launch per call)")
+            us = lambda v: round(float(v) / 1e3 / k, 3)  # noqa: E731  (ns summed -> us per proposal)
+            ev, ip = dt[0], dt[3]
+            res["breakdown_us_per_proposal"] = {
+                "td_evaluate": us(ev), "evaluate_classify": us(dt[1]), "evaluate_server_round_trip": us(dt[2]),
+                "evaluate_rest": us(ev - dt[1] - dt[2]),
+                "td_interpolate_1pt": us(ip), "interpolate_classify": us(dt[4]),
+                "interpolate_server_round_trip": us(dt[5]), "interpolate_rest": us(ip - dt[4] - dt[5]),
+                "host_loop_modeln_copy": us(dt[9]), "host_loop_rest": us(dt[10] - ev - ip - dt[9]),
+                "calls_per_proposal": {"td_evaluate": round(float(dt[6]) / k, 3),
+                                       "td_interpolate": round(float(dt[7]) / k, 3),
+                                       "full_evaluates": int(dt[8])}}
         ctx.timing(enable=False)
         out[name] = res
         ch.close()

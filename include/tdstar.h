@@ -298,6 +298,40 @@ int td_swap_decide(int64_t R, const double *phis, const int64_t *levels, const d
 int td_rounds_temper(td_rounds *r, int64_t M, int64_t K, const double *temps, int64_t *levels, int64_t rnd0,
                      uint64_t seed, double *phis_out, int64_t *levels_out, int64_t *tried, int64_t *accepted);
 
+/* ------------------------------------------------------------------------
+ * The exchange across GPUs (one replica per GPU, an RCCL allgather
+ * over xGMI for the swap step).  A td_comm is an RCCL communicator of the
+ * job's ranks: rank 0 makes the id (td_comm_unique_id) and the caller ships
+ * it to every rank (e.g. torch.distributed); td_comm_create blocks until all
+ * ranks joined.  td_comm_allgather: count doubles from every rank, host
+ * buffers (out[nranks * count], rank order). */
+#define TD_COMM_ID_BYTES 128
+typedef struct td_comm td_comm;
+int td_comm_unique_id(uint8_t *id /* TD_COMM_ID_BYTES */);
+int td_comm_create(td_comm **out, int device, int nranks, int rank, const uint8_t *id);
+int td_comm_allgather(td_comm *c, const double *in, int64_t count, double *out);
+int td_comm_destroy(td_comm *c);
+/* M rounds of parallel tempering with no host in the loop: the chains of r
+ * (this rank's replicas, replica g = rank * nchains + k; every rank holds as
+ * many) run in ONE launch; after every K proposals each publishes its exact
+ * phi to device memory, an allgather on the communicator's stream (issued
+ * ahead, each waiting on a flag the kernel raises: hipStreamWaitValue64)
+ * brings every replica's phi, and every workgroup decides the round's swaps
+ * itself (td_swap_decide's rule) and takes its chain's new temperature.
+ * comm NULL: one rank holds every replica (the phis meet in device memory, no
+ * collective).  Same trace as td_rounds_temper over the same replicas: the
+ * host replays every decision on the logged phis and fails (TD_ERR_HIP) if
+ * the device's differ.  levels[R] in/out, phis_out / levels_out [M x R],
+ * tried / accepted [R-1] added to (all nullable but levels); R <= 64.
+ * timing_out[7] (nullable, s): the call, launch issued, exchanges enqueued;
+ * per round (means, workgroup 0's wall clock): the exchange (this rank's phis
+ * all in -> every phi gathered), the proposals (gathered -> its next phi),
+ * the wait for the rank's slowest replica (its phi -> the rank's last); the
+ * kernel's span from its first publish to its last gather. */
+int td_rounds_exchange(td_rounds *r, td_comm *comm, int64_t M, int64_t K, const double *temps, int64_t *levels,
+                       int64_t rnd0, uint64_t seed, double *phis_out, int64_t *levels_out, int64_t *tried,
+                       int64_t *accepted, double *timing_out);
+
 #ifdef __cplusplus
 }
 #endif

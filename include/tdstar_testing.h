@@ -71,6 +71,15 @@ int tdt_set_server_post_delay(int ms);
  * runs each round once, with the results of an undisturbed launch.  One-shot;
  * ends the running launch. */
 int tdt_rounds_force_exit(td_rounds *r, const int32_t *slots, int64_t nslots);
+/* Diagnostic: the drop-in path's wall time per stage, ns, accumulated on the
+ * context (then zeroed if reset): [0] td_evaluate, [1] its model
+ * classification (which state the caller's cells are an edit of), [2] its
+ * resident server's round trip (post -> answer), [3] td_interpolate of one
+ * point, [4] its classification, [5] its server round trip, [6] td_evaluate
+ * calls, [7] 1-point td_interpolate calls, [8] full evaluates, [9] a DROPIN
+ * chain's modeln copies (the host loop's deepcopy), [10] its iterations'
+ * time, [11] its iterations. */
+int tdt_dropin_timing(td_ctx *ctx, int reset, int64_t out[12]);
 /* The block-wide exact sequential sum (exact_sum.h, used for chi^2 over long
  * ray lists): prefix[k] = C0 + term[0] + ... + term[k] added strictly left to
  * right in FP64 (MCsub.jl:170-172).  *fast = 1 when the parallel path proved
@@ -100,9 +109,9 @@ int tdt_wave_seq_sum(int device, const double *term, int64_t cnt, double C0, dou
                      int *fallbacks);
 
 /* chi^2 (MCsub.jl:169-172) of a caller-given ptS[n] against the context's tS
- * and allSig, through the device code that computes it in the product:
- * path 0 the fused tail of td_evaluate's ray-sum kernel (n <= 2048), 1 the
- * block-wide exact scan td_evaluate uses for long ray lists, 2 the device
+ * and allSig, through the code that computes it in the product: path 0
+ * td_evaluate's (the host adds the terms in k order where the kernel put
+ * ptS), 1 the block-wide exact scan of td_misfit (k_chi2), 2 the device
  * chain's starting-state prefix sums (k_chi2_prefix), 3 the chain's
  * proposal-time one-wave scan (from k0 = 0 -> out[0], and restarted at
  * k0 = n/2 on path 2's prefix -> out[1]).  Lets the tests pin the HIP code to

@@ -18,7 +18,7 @@ from .data import (CONFIGS, ak135_slowness, box, interp1, load_data_Tonga, lonla
                    random_model, segments, synthetic_rays)
 from .defstruct import DataStruct, Model, Ray  # noqa: F401
 from .forward import Interpolation, TdContext, context_for, evaluate, v_nearest  # noqa: F401
-from .tempering import Exchange, TemperingLadder, decide_swaps, geometric_ladder  # noqa: F401
+from .tempering import Exchange, NativeComm, TemperingLadder, decide_swaps, geometric_ladder  # noqa: F401
 from .posterior import plot_model_hist, section  # noqa: F401
 from .sharded import RayShardedContext, ray_points, shard_rays, sub_datastruct  # noqa: F401
 from . import jld  # noqa: F401  (save/load model.jld, main_inversion.jl:18)

@@ -61,6 +61,12 @@ SIGNATURES = {
     "td_swap_decide": (ctypes.c_int, [_i64, _pd, _pi64, _pd, _i64, ctypes.c_uint64, _pi64, _pi64, _pi64]),
     "td_rounds_temper": (ctypes.c_int, [_vp, _i64, _i64, _pd, _pi64, _i64, ctypes.c_uint64, _pd, _pi64, _pi64,
                                         _pi64]),
+    "td_rounds_exchange": (ctypes.c_int, [_vp, _vp, _i64, _i64, _pd, _pi64, _i64, ctypes.c_uint64, _pd, _pi64,
+                                          _pi64, _pi64, _pd]),
+    "td_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "td_comm_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
+    "td_comm_allgather": (ctypes.c_int, [_vp, _pd, _i64, _pd]),
+    "td_comm_destroy": (ctypes.c_int, [_vp]),
     "td_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "td_timing_reset": (ctypes.c_int, [_vp]),
     "td_timing_get": (ctypes.c_int, [_vp, ctypes.c_char_p, _pi64, _pd]),
@@ -100,6 +106,7 @@ SIGNATURES = {
     "tdt_set_incremental": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_set_server_post_delay": (ctypes.c_int, [ctypes.c_int]),
     "tdt_rounds_force_exit": (ctypes.c_int, [_vp, _pi32, _i64]),
+    "tdt_dropin_timing": (ctypes.c_int, [_vp, ctypes.c_int, _pi64]),
     "tdt_shadow_diag": (ctypes.c_int, [_vp, _pi64]),
     "tdt_shadow_profile": (ctypes.c_int, [_vp, _pi64]),
     "tdt_chi2": (ctypes.c_int, [_vp, _pd, ctypes.c_int, _pd]),

@@ -2,6 +2,7 @@
 // interpolate.  Host-side glue only; the arithmetic is in kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -188,6 +189,22 @@ hipError_t nearest_uploaded(td_ctx *ctx, const double *qx, const double *qy, con
                           ctx->num_cus, best_i, best_d, zeta0, ctx->stream, tm);
 }
 
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// MCsub.jl:169-172: C = 0; for k in 1:n, C += ((ptS - tS)[k]^2 * 1.0) / allSig[k]^2 -- strictly in k
+// order, each operation an IEEE double one (no contraction: -ffp-contract=off), as the reference's loop.
+double host_chi2(const double *ptS, const double *tS, const double *sig, int64_t n) {
+    double C = 0.0;
+    for (int64_t k = 0; k < n; ++k) {
+        const double d = ptS[k] - tS[k];
+        C = C + ((d * d) * 1.0) / (sig[k] * sig[k]);
+    }
+    return C;
+}
+
 int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                   int64_t ncells, double *ptS_out, double *phi_out, int32_t *nearest_out) {
     int rc = upload_cells(ctx, x, y, z, zeta, ncells);
@@ -196,14 +213,16 @@ int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
     hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, ncells, ctx->best_i, ctx->best_d, ctx->zeta0);
     if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
-    // [phi, ptS] land in pinned host memory straight from the kernel (no copy back)
-    e = launch_ray_sums_chi2(g, ctx->zeta0, ctx->ptS, ctx->phi, ctx->stream, tm, ctx->h_out_dev);
-    if (e != hipSuccess) return hip_err(ctx, e, "ray-sum / chi2 kernel");
+    // ptS lands in pinned host memory straight from the kernel (no copy back)
+    e = launch_ray_sums(g, ctx->zeta0, ctx->ptS, ctx->stream, tm, ctx->h_out_dev + 1);
+    if (e != hipSuccess) return hip_err(ctx, e, "ray-sum kernel");
     if (nearest_out && g.P)
         TD_HIP(ctx, hipMemcpyAsync(ctx->h_best_i, ctx->best_i, sizeof(int) * (size_t)g.P, hipMemcpyDeviceToHost,
                                    ctx->stream));
     TD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (phi_out) *phi_out = ctx->h_out[0];
+    // chi^2: the n terms added in k order by the host, where ptS already is (MCsub.jl:169-172)
+    const double phi = host_chi2(ctx->h_out + 1, ctx->tS_host.data(), ctx->sig_host.data(), g.n);
+    if (phi_out) *phi_out = phi;
     if (ptS_out && g.n) std::memcpy(ptS_out, ctx->h_out + 1, sizeof(double) * (size_t)g.n);
     if (nearest_out && g.P) std::memcpy(nearest_out, ctx->h_best_i, sizeof(int) * (size_t)g.P);
     return TD_OK;
@@ -317,6 +336,7 @@ int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, 
     c->hy = hy;
     c->hz = hz;
     c->sig_host.assign(allSig ? allSig : nullptr, allSig ? allSig + n : nullptr);
+    c->tS_host.assign(tS ? tS : nullptr, tS ? tS + n : nullptr);
     c->likelihood = likelihood_constant(c->sig_host.data(), n);
 
     auto dalloc = [&](void **p, size_t bytes, const char *what) -> int {
@@ -459,11 +479,14 @@ int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const dou
     if (nCells < 0 || (nCells > 0 && (!xCell || !yCell || !zCell || !zeta)))
         return set_err(ctx, TD_ERR_ARG, "td_evaluate: bad cell arrays");
     if (nCells > 0x7fffffff) return set_err(ctx, TD_ERR_ARG, "td_evaluate: too many cells");
+    const int64_t t0 = now_ns();
     TD_HIP(ctx, hipSetDevice(ctx->device));
     servers_quiesce((nearest_out || !ctx->incremental) ? nullptr : shadow_chain_of(ctx));
     int rc = (nearest_out || !ctx->incremental)
                  ? evaluate_full(ctx, xCell, yCell, zCell, zeta, nCells, ptS_out, phi_out, nearest_out)
                  : evaluate_incremental(ctx, xCell, yCell, zCell, zeta, nCells, ptS_out, phi_out);
+    ctx->dropin_ns[0] += now_ns() - t0;
+    ctx->dropin_ns[6] += 1;
     if (rc) return rc;
     if (likelihood_out) *likelihood_out = ctx->likelihood;  // MCsub.jl:179-182: model-independent
     return TD_OK;
@@ -505,9 +528,12 @@ int td_interpolate(td_ctx *ctx, const double *xCell, const double *yCell, const 
     if (np == 0) return TD_OK;
     TD_HIP(ctx, hipSetDevice(ctx->device));
     if (np == 1 && !nearest_out && ctx->incremental && nCells > 0) {  // a chain's 1-point query (:81, :146)
+        const int64_t t0 = now_ns();
         servers_quiesce(shadow_chain_of(ctx));
         int handled = 0;
         int rc = interpolate_incremental(ctx, xCell, yCell, zCell, zeta, nCells, X[0], Y[0], Z[0], zeta_out, &handled);
+        ctx->dropin_ns[3] += now_ns() - t0;
+        ctx->dropin_ns[7] += 1;
         if (rc) return rc;
         if (handled) return TD_OK;
     }
@@ -643,7 +669,12 @@ int tdt_block_delta_sum(int device, const double *term, const double *term_old, 
 int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]) {
     if (!ctx || !out || (!ptS && ctx->g.n > 0) || path < 0 || path > 3) return set_err(ctx, TD_ERR_ARG, "tdt_chi2");
     const int64_t n = ctx->g.n;
-    if (n < 1 || n > 4096 || (path == 0 && n > 2048)) return set_err(ctx, TD_ERR_ARG, "tdt_chi2: n out of range");
+    if (n < 1 || n > 4096) return set_err(ctx, TD_ERR_ARG, "tdt_chi2: n out of range");
+    if (path == 0) {  // td_evaluate's: the host's sequential sum
+        out[0] = host_chi2(ptS, ctx->tS_host.data(), ctx->sig_host.data(), n);
+        out[1] = 0.0;
+        return TD_OK;
+    }
     TD_HIP(ctx, hipSetDevice(ctx->device));
     double *dp = nullptr, *scratch = nullptr, *dout = nullptr;
     const size_t sn = 3 * (size_t)n + 8 + 1024 / sizeof(double);
@@ -653,8 +684,8 @@ int tdt_chi2(td_ctx *ctx, const double *ptS, int path, double out[2]) {
     if (e == hipSuccess) e = hipMemsetAsync(dout, 0, sizeof(double) * 2, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(dp, ptS, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess) {
-        if (path <= 1)
-            e = test_chi2(dp, ctx->g.tS, ctx->g.sig, (int)n, path, scratch, dout, ctx->stream);
+        if (path == 1)
+            e = test_chi2(dp, ctx->g.tS, ctx->g.sig, (int)n, scratch, dout, ctx->stream);
         else
             e = test_chain_chi2(dp, ctx->g.tS, ctx->g.sig, (int)n, path, scratch, dout, ctx->stream);
     }

@@ -26,6 +26,7 @@
 #include "../../include/tdstar_testing.h"
 #include "chain_dev.h"
 #include "chain_logic.h"
+#include "comm.h"
 #include "ctx.h"
 
 using namespace tdstar;
@@ -73,6 +74,21 @@ struct td_rounds {
     double tr_first = 0.0, tr_last = 0.0;  // diagnostic (TD_ROUNDS_TRACE): summed arrival times, rounds
     long long tr_n = 0;
     std::vector<char> force_exit;  // testing (tdt_rounds_force_exit): one-shot, per chain
+    // exchange rounds (td_rounds_exchange, chain_dev.h RoundX): buffers made on first use
+    int x_R = 0;                  // replicas the buffers are sized for
+    double *x_in = nullptr, *x_out = nullptr, *x_temps = nullptr;  // device
+    unsigned long long *x_rdy = nullptr, *x_gdone = nullptr;       // device
+    unsigned long long *x_ready = nullptr;                         // signal memory (or pinned, host trigger)
+    bool x_ready_pinned = false;
+    int *x_lev = nullptr;                                          // device [local][R]
+    double *x_log_phi = nullptr;                                   // pinned [M][R]
+    int *x_log_lev = nullptr;                                      // pinned [M][R]
+    long long *x_log_t = nullptr;                                  // pinned [M][3]
+    long long *x_err = nullptr;                                    // pinned
+    int64_t x_log_cap = 0;        // rounds the logs hold
+    RoundX x_host{};              // the launch's exchange descriptor, and its device copy
+    RoundX *x_desc = nullptr;
+    unsigned long long x_tag = 0, x_gtag = 0;  // rounds exchanged so far (the flags' bases)
 };
 
 namespace {
@@ -190,6 +206,7 @@ int host_iteration(td_chain *ch) {
         tdchain::birth_zeta(P, p, czeta);
     }
     if (!p.valid) return TD_OK;
+    const int64_t tcopy = now_ns();
     std::vector<double> nx = ch->x, ny = ch->y, nz = ch->z, nzeta = ch->zeta;  // modeln = deepcopy(model)
     switch (p.action) {
         case tdchain::kBirth:  // :85-88 append!
@@ -202,6 +219,7 @@ int host_iteration(td_chain *ch) {
         case tdchain::kChange: nzeta[k] = p.zeta; break;  // :189
         case tdchain::kMove: nx[k] = p.x; ny[k] = p.y; nz[k] = p.z; break;  // :234-236
     }
+    ch->ctx->dropin_ns[9] += now_ns() - tcopy;
     double phi_n = 0.0;
     std::vector<double> ptS_n(ch->ptS.size());
     int rc = host_evaluate(ch, nx, ny, nz, nzeta, &phi_n, ptS_n.data());
@@ -708,7 +726,9 @@ int td_rounds_create(td_rounds **out, td_chain *const *chains, int64_t nchains) 
     }
     if (e == hipSuccess) e = hipMalloc(&r->desc_dev, sizeof(DevChain) * (size_t)nchains);
     if (e == hipSuccess) e = hipHostMalloc(&r->desc_host, sizeof(DevChain) * (size_t)nchains, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    // the resident launch on a hardware queue of its own: it must not hold back other streams
+    // (torch's, RCCL's exchange stream) that HIP would otherwise deal onto its queue
+    if (e == hipSuccess) e = rounds_stream(&r->stream, c->device);
     if (e != hipSuccess) {
         (void)td_rounds_destroy(r);
         return hip_err(c, e, "td_rounds_create");
@@ -827,20 +847,6 @@ int td_rounds_run(td_rounds *r, int64_t K, const double *temps, double *phi_out)
     return TD_OK;
 }
 
-namespace {
-// tempering.py _mix64 / _uniform: SplitMix64's finaliser over (seed, round, level)
-uint64_t swap_mix64(uint64_t x) {
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-double swap_uniform(uint64_t seed, uint64_t rnd, uint64_t level) {
-    uint64_t x = swap_mix64(seed * 0x9E3779B97F4A7C15ull + rnd);
-    x = swap_mix64(x + level * 0xD1B54A32D192ED03ull + 1ull);
-    return ((double)(x >> 12) + 0.5) / 4503599627370496.0;  // (k + 1/2) / 2^52: in (0, 1), exact
-}
-}  // namespace
-
 int td_swap_decide(int64_t R, const double *phis, const int64_t *levels, const double *temps, int64_t rnd,
                    uint64_t seed, int64_t *new_levels, int64_t *tried, int64_t *accepted) {
     if (R < 1 || !phis || !levels || !temps || !new_levels || rnd < 0) return TD_ERR_ARG;
@@ -853,10 +859,8 @@ int td_swap_decide(int64_t R, const double *phis, const int64_t *levels, const d
     for (int64_t l = rnd % 2; l < R - 1; l += 2) {
         const int64_t a = owner[(size_t)l], b = owner[(size_t)l + 1];
         if (tried) tried[l] += 1;
-        // tempering.py swap_log_alpha, the same operations (no contraction: -ffp-contract=off)
-        const double la = (phis[a] - phis[b]) * (1.0 / (2.0 * temps[l]) - 1.0 / (2.0 * temps[l + 1]));
-        const double u = swap_uniform(seed, (uint64_t)rnd, (uint64_t)l);
-        if (la >= 0.0 || (u > 0.0 && std::log(u) < la)) {  // (the host libm log, as Python's math.log)
+        // chain_logic.h swap_accept: what the exchange kernel decides with (no contraction: -ffp-contract=off)
+        if (tdchain::swap_accept(phis[a], phis[b], temps[l], temps[l + 1], seed, (uint64_t)rnd, (uint64_t)l)) {
             new_levels[a] = l + 1;
             new_levels[b] = l;
             owner[(size_t)l] = b;
@@ -895,14 +899,278 @@ int td_rounds_temper(td_rounds *r, int64_t M, int64_t K, const double *temps, in
     return TD_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+void exchange_free(td_rounds *r) {
+    for (void *p : {(void *)r->x_in, (void *)r->x_out, (void *)r->x_temps, (void *)r->x_rdy, (void *)r->x_gdone,
+                    (void *)r->x_lev, (void *)r->x_desc})
+        if (p) (void)hipFree(p);
+    if (r->x_ready) (void)(r->x_ready_pinned ? hipHostFree(r->x_ready) : hipFree(r->x_ready));
+    for (void *p : {(void *)r->x_log_phi, (void *)r->x_log_lev, (void *)r->x_log_t, (void *)r->x_err})
+        if (p) (void)hipHostFree(p);
+    r->x_in = r->x_out = r->x_temps = nullptr;
+    r->x_rdy = r->x_gdone = r->x_ready = nullptr;
+    r->x_lev = nullptr;
+    r->x_desc = nullptr;
+    r->x_log_phi = nullptr;
+    r->x_log_lev = nullptr;
+    r->x_log_t = nullptr;
+    r->x_err = nullptr;
+    r->x_R = 0;
+    r->x_log_cap = 0;
+    r->x_tag = r->x_gtag = 0;
+}
+
+// TD_EXCHANGE_TRIGGER=host: the host watches `ready` (pinned memory) and issues each allgather itself,
+// instead of the exchange stream waiting on it (hipStreamWaitValue64) -- a diagnostic alternative
+bool exchange_host_trigger() {
+    static const bool on = [] {
+        const char *e = std::getenv("TD_EXCHANGE_TRIGGER");
+        return e && std::strcmp(e, "host") == 0;
+    }();
+    return on;
+}
+
+int exchange_alloc(td_rounds *r, int R, int64_t M) {
+    td_ctx *c = r->ctx;
+    const int local = (int)r->chains.size();
+    if (r->x_R != R) {
+        exchange_free(r);
+        TD_HIP(c, hipMalloc(&r->x_in, sizeof(double) * (size_t)local));
+        TD_HIP(c, hipMalloc(&r->x_out, sizeof(double) * (size_t)R));
+        TD_HIP(c, hipMalloc(&r->x_temps, sizeof(double) * (size_t)R));
+        TD_HIP(c, hipMalloc(&r->x_rdy, sizeof(unsigned long long) * (size_t)local));
+        TD_HIP(c, hipMalloc(&r->x_gdone, sizeof(unsigned long long)));
+        TD_HIP(c, hipMalloc(&r->x_lev, sizeof(int) * (size_t)local * (size_t)R));
+        TD_HIP(c, hipMalloc(&r->x_desc, sizeof(RoundX)));
+        TD_HIP(c, hipMemset(r->x_rdy, 0, sizeof(unsigned long long) * (size_t)local));
+        TD_HIP(c, hipMemset(r->x_gdone, 0, sizeof(unsigned long long)));
+        r->x_ready_pinned = exchange_host_trigger();
+        if (r->x_ready_pinned) {
+            TD_HIP(c, hipHostMalloc(&r->x_ready, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent));
+        } else {  // what hipStreamWaitValue64 waits on
+            TD_HIP(c, hipExtMallocWithFlags(reinterpret_cast<void **>(&r->x_ready), sizeof(unsigned long long),
+                                            hipMallocSignalMemory));
+        }
+        *reinterpret_cast<volatile unsigned long long *>(r->x_ready) = 0;  // (host-visible either way)
+        TD_HIP(c, hipHostMalloc(&r->x_err, sizeof(long long), hipHostMallocMapped | hipHostMallocCoherent));
+        r->x_R = R;
+        r->x_tag = r->x_gtag = 0;
+    }
+    if (M > r->x_log_cap) {
+        if (r->x_log_phi) (void)hipHostFree(r->x_log_phi);
+        if (r->x_log_lev) (void)hipHostFree(r->x_log_lev);
+        if (r->x_log_t) (void)hipHostFree(r->x_log_t);
+        r->x_log_phi = nullptr;
+        r->x_log_lev = nullptr;
+        r->x_log_t = nullptr;
+        r->x_log_cap = 0;
+        TD_HIP(c, hipHostMalloc(&r->x_log_phi, sizeof(double) * (size_t)M * (size_t)R, hipHostMallocMapped));
+        TD_HIP(c, hipHostMalloc(&r->x_log_lev, sizeof(int) * (size_t)M * (size_t)R, hipHostMallocMapped));
+        TD_HIP(c, hipHostMalloc(&r->x_log_t, sizeof(long long) * 3 * (size_t)M, hipHostMallocMapped));
+        r->x_log_cap = M;
+    }
+    return TD_OK;
+}
+
+template <class T>
+T *dev_addr(T *host) {  // the device address of mapped pinned memory
+    void *d = nullptr;
+    return hipHostGetDevicePointer(&d, host, 0) == hipSuccess ? static_cast<T *>(d) : nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int td_rounds_exchange(td_rounds *r, td_comm *comm, int64_t M, int64_t K, const double *temps, int64_t *levels,
+                       int64_t rnd0, uint64_t seed, double *phis_out, int64_t *levels_out, int64_t *tried,
+                       int64_t *accepted, double *timing_out) {
+    if (!r || M < 0 || K <= 0 || K > INT32_MAX || M * K > ((int64_t)1 << 40) || !temps || !levels || rnd0 < 0)
+        return set_err(r ? r->ctx : nullptr, TD_ERR_ARG, "td_rounds_exchange");
+    td_ctx *c = r->ctx;
+    const int local = (int)r->chains.size();
+    if (local == 0) return set_err(c, TD_ERR_ARG, "td_rounds_exchange: its chains were destroyed");
+    const int nranks = comm ? comm->nranks : 1, rank = comm ? comm->rank : 0;
+    const int64_t R = (int64_t)local * nranks;
+    if (R > 64) return set_err(c, TD_ERR_ARG, "td_rounds_exchange: at most 64 replicas (one lane each)");
+    if (comm && comm->device != c->device)
+        return set_err(c, TD_ERR_ARG, "td_rounds_exchange: the communicator is on another device");
+    {
+        std::vector<char> seen((size_t)R, 0);
+        for (int64_t g = 0; g < R; ++g) {
+            if (levels[g] < 0 || levels[g] >= R || seen[(size_t)levels[g]])
+                return set_err(c, TD_ERR_ARG, "td_rounds_exchange: levels are not a permutation");
+            seen[(size_t)levels[g]] = 1;
+        }
+        for (int64_t l = 0; l < R; ++l)
+            if (!(temps[l] > 0.0)) return set_err(c, TD_ERR_ARG, "td_rounds_exchange: need T > 0");
+    }
+    if (M == 0) return TD_OK;
+    const auto t_call = std::chrono::steady_clock::now();
+    TD_HIP(c, hipSetDevice(c->device));
+    servers_quiesce(nullptr);  // (ends this launch's host-posted rounds too)
+    int rc = exchange_alloc(r, (int)R, M);
+    if (rc) return rc;
+    // every chain starts at its level's temperature; the kernel's workgroups each keep all levels
+    std::vector<int> lev0((size_t)local * (size_t)R);
+    std::vector<int64_t> iter0((size_t)local);
+    for (int k = 0; k < local; ++k) {
+        iter0[(size_t)k] = r->chains[(size_t)k]->iter;
+        td_chain *ch = r->chains[(size_t)k];
+        ch->prm.temperature = temps[levels[rank * local + k]];
+        ch->P.temperature = ch->prm.temperature;
+        tdchain::params_derived(ch->P);
+        ch->dev.params = ch->P;
+        r->desc_host[k] = ch->dev;
+        ch->desc_dirty = true;  // (its own descriptor copy is refreshed on its next run)
+        for (int64_t g = 0; g < R; ++g) lev0[(size_t)k * (size_t)R + (size_t)g] = (int)levels[g];
+    }
+    *reinterpret_cast<volatile long long *>(r->x_err) = 0;
+    TD_HIP(c, hipMemcpyAsync(r->x_lev, lev0.data(), sizeof(int) * lev0.size(), hipMemcpyHostToDevice, r->stream));
+    TD_HIP(c, hipMemcpyAsync(r->x_temps, temps, sizeof(double) * (size_t)R, hipMemcpyHostToDevice, r->stream));
+    TD_HIP(c, hipMemcpyAsync(r->desc_dev, r->desc_host, sizeof(DevChain) * (size_t)local, hipMemcpyHostToDevice,
+                             r->stream));
+    RoundX &x = r->x_host;
+    x = RoundX{};
+    x.xin = r->x_in;
+    x.xout = comm ? r->x_out : r->x_in;
+    x.rdy = r->x_rdy;
+    x.ready = r->x_ready_pinned ? dev_addr(r->x_ready) : r->x_ready;
+    x.gdone = comm ? r->x_gdone : nullptr;
+    x.ready_base = r->x_tag;
+    x.gdone_base = r->x_gtag;
+    x.lev = r->x_lev;
+    x.temps = r->x_temps;
+    x.log_phi = dev_addr(r->x_log_phi);
+    x.log_lev = dev_addr(r->x_log_lev);
+    x.log_t = dev_addr(r->x_log_t);
+    x.err = dev_addr(r->x_err);
+    x.rnd0 = rnd0;
+    x.seed = seed;
+    x.R = (int)R;
+    x.local = local;
+    x.rank = rank;
+    x.M = (int)M;
+    x.K = (int)K;
+    if (!x.ready || !x.log_phi || !x.log_lev || !x.log_t || !x.err)
+        return set_err(c, TD_ERR_HIP, "td_rounds_exchange: pinned memory without a device address");
+    TD_HIP(c, hipMemcpyAsync(r->x_desc, &r->x_host, sizeof(RoundX), hipMemcpyHostToDevice, r->stream));
+    ScriptArgs sa{};
+    sa.rx = r->x_desc;
+    hipError_t e = chain_run(r->desc_host, r->desc_dev, local, M * K, r->stream, &sa,
+                             DrawsBuf{&c->draws, &c->draws_bytes});
+    if (e != hipSuccess) return hip_err(c, e, "k_chain_run launch (exchange rounds)");
+    const auto t_launched = std::chrono::steady_clock::now();
+    // the exchanges: each allgather on the exchange stream once this rank's phis of the round are in
+    bool stuck = false;
+    if (comm) {
+        for (int64_t j = 0; j < M && !stuck; ++j) {
+            const unsigned long long tag = r->x_tag + (unsigned long long)j + 1ull;
+            if (r->x_ready_pinned) {  // host trigger
+                const auto t0 = std::chrono::steady_clock::now();
+                for (long long spin = 0; *reinterpret_cast<volatile unsigned long long *>(r->x_ready) < tag; ++spin)
+                    if ((spin & 1023) == 1023 &&
+                        (*reinterpret_cast<volatile long long *>(r->x_err) ||
+                         std::chrono::steady_clock::now() - t0 > std::chrono::seconds(12))) {
+                        stuck = true;
+                        break;
+                    }
+                if (stuck) break;
+            } else {
+                e = hipStreamWaitValue64(comm->stream, r->x_ready, tag, hipStreamWaitValueGte);
+                if (e != hipSuccess) return hip_err(c, e, "hipStreamWaitValue64");
+            }
+            const ncclResult_t nr = ncclAllGather(r->x_in, r->x_out, (size_t)local, ncclFloat64, comm->comm, comm->stream);
+            if (nr != ncclSuccess) return set_err(c, TD_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+            e = hipStreamWriteValue64(comm->stream, r->x_gdone, r->x_gtag + (unsigned long long)j + 1ull, 0);
+            if (e != hipSuccess) return hip_err(c, e, "hipStreamWriteValue64");
+        }
+    }
+    const auto t_enqueued = std::chrono::steady_clock::now();
+    e = hipStreamSynchronize(r->stream);  // (the kernel gives up after 10 s without an exchange)
+    if (e != hipSuccess) return hip_err(c, e, "exchange rounds");
+    const bool failed = *reinterpret_cast<volatile long long *>(r->x_err) != 0 || stuck;
+    if (comm) {
+        if (failed && !r->x_ready_pinned) {  // release the exchange stream's waits, then drain it
+            e = hipStreamWriteValue64(r->stream, r->x_ready, ~0ull >> 1, 0);
+            if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+        }
+        e = hipStreamSynchronize(comm->stream);
+        if (e != hipSuccess) return hip_err(c, e, "exchange stream");
+    }
+    const auto t_done = std::chrono::steady_clock::now();
+    for (int k = 0; k < local; ++k) {
+        td_chain *ch = r->chains[(size_t)k];
+        adopt_scalars(ch);
+        ch->stats.iterations += ch->iter - iter0[(size_t)k];
+    }
+    if (failed) {
+        exchange_free(r);  // (fresh flags next time)
+        return set_err(c, TD_ERR_HIP, "td_rounds_exchange: an exchange never came (10 s)");
+    }
+    // the host replays every round's decisions on the logged phis: the device's levels must be its
+    std::vector<int64_t> lv(levels, levels + R), nl((size_t)R);
+    for (int64_t j = 0; j < M; ++j) {
+        const double *ph = r->x_log_phi + j * R;
+        if (td_swap_decide(R, ph, lv.data(), temps, rnd0 + j, seed, nl.data(), tried, accepted))
+            return set_err(c, TD_ERR_ARG, "td_rounds_exchange: levels");
+        for (int64_t g = 0; g < R; ++g)
+            if (nl[(size_t)g] != r->x_log_lev[j * R + g])
+                return set_err(c, TD_ERR_HIP, "td_rounds_exchange: the device's swap decisions differ from the host's");
+        lv = nl;
+        if (phis_out) std::memcpy(phis_out + j * R, ph, sizeof(double) * (size_t)R);
+        if (levels_out) std::memcpy(levels_out + j * R, lv.data(), sizeof(int64_t) * (size_t)R);
+    }
+    for (int64_t g = 0; g < R; ++g) levels[g] = lv[(size_t)g];
+    for (int k = 0; k < local; ++k) {  // each chain leaves at its final level's temperature
+        td_chain *ch = r->chains[(size_t)k];
+        const double phi = r->x_log_phi[(M - 1) * R + rank * local + k];
+        if (phi != ch->phi) return set_err(c, TD_ERR_HIP, "td_rounds_exchange: a published phi is not the chain's");
+        ch->prm.temperature = temps[lv[(size_t)(rank * local + k)]];
+        ch->P.temperature = ch->prm.temperature;
+        tdchain::params_derived(ch->P);
+        ch->dev.params = ch->P;
+        ch->desc_dirty = true;
+    }
+    r->x_tag += (unsigned long long)M;
+    r->x_gtag += (unsigned long long)M;
+    if (timing_out) {
+        // [0] the call, s; [1] launch issued, s; [2] exchanges enqueued, s; [3] mean time from this rank's phis
+        // all in (workgroup 0 saw every local flag) to every phi gathered: the exchange; [4] mean time from
+        // the phis gathered to workgroup 0's next phi (its proposals); [5] mean time from workgroup 0's phi to
+        // the rank's last (waiting for the slowest local replica); [6] the kernel's first publish to its last
+        // gather, s
+        double ex = 0.0, pr = 0.0, lw = 0.0;
+        const long long *t = r->x_log_t;
+        for (int64_t j = 0; j < M; ++j) {
+            ex += (double)(t[3 * j + 2] - t[3 * j + 1]);
+            lw += (double)(t[3 * j + 1] - t[3 * j]);
+            if (j > 0) pr += (double)(t[3 * j] - t[3 * j - 1]);
+        }
+        const double tick = 1e-8;  // the 100 MHz wall clock
+        timing_out[0] = std::chrono::duration<double>(t_done - t_call).count();
+        timing_out[1] = std::chrono::duration<double>(t_launched - t_call).count();
+        timing_out[2] = std::chrono::duration<double>(t_enqueued - t_call).count();
+        timing_out[3] = ex / (double)M * tick;
+        timing_out[4] = M > 1 ? pr / (double)(M - 1) * tick : 0.0;
+        timing_out[5] = lw / (double)M * tick;
+        timing_out[6] = (double)(t[3 * (M - 1) + 2] - t[0]) * tick;
+    }
+    return TD_OK;
+}
+
 int td_rounds_destroy(td_rounds *r) {
     if (!r) return TD_OK;
     if (rounds_trace() && r->tr_n > 0)
         std::fprintf(stderr, "[rounds_trace] %d replicas, %lld rounds: first done %.2f us, last done %.2f us after the post\n",
                      (int)r->chains.size(), (long long)r->tr_n, r->tr_first / r->tr_n, r->tr_last / r->tr_n);
+    exchange_free(r);
     int rc = rounds_stop(r);
     for (td_chain *ch : r->chains) ch->rounds = nullptr;
-    if (r->stream) (void)hipStreamDestroy(r->stream);
+    if (r->stream) (void)hipStreamSynchronize(r->stream);  // (the process's rounds stream: kept)
     if (r->rb_host) (void)hipHostFree(r->rb_host);
     if (r->desc_dev) (void)hipFree(r->desc_dev);
     if (r->desc_host) (void)hipHostFree(r->desc_host);
@@ -979,10 +1247,13 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
     if (e != hipSuccess) return hip_err(ch->ctx, e, "hipSetDevice");
     if (ch->engine != TD_ENGINE_DROPIN) servers_quiesce(nullptr);  // DROPIN's td_evaluate keeps its own
     if (ch->engine != TD_ENGINE_DEVICE) {
+        const int64_t t0 = now_ns();
         for (int64_t i = 0; i < iterations; ++i) {
             int rc = host_iteration(ch);
             if (rc) return rc;
         }
+        ch->ctx->dropin_ns[10] += now_ns() - t0;
+        ch->ctx->dropin_ns[11] += iterations;
         ch->stats.phi = ch->phi;
         ch->stats.ncells = (int64_t)ch->x.size();
         return TD_OK;
@@ -1255,7 +1526,9 @@ int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int 
         for (int k = 0; k < nsteps; ++k) m->step[k] = st[k];
         const ScriptStep held = ch->srv_pending;
         const bool had = ch->srv_has_pending;
+        const int64_t t0 = now_ns();
         rc = server_post(ch);
+        ch->ctx->dropin_ns[2] += now_ns() - t0;
         if (rc == TD_OK) {
             ch->srv_pending = st[nsteps - 1];
             ch->srv_has_pending = st[nsteps - 1].decision == kDecideLater;
@@ -1291,7 +1564,9 @@ int shadow_server_query(td_chain *ch, double x, double y, double z, const Script
     m->q[2] = z;
     m->has_edit = edit ? 1 : 0;
     if (edit) m->qedit = *edit;
+    const int64_t t0 = now_ns();
     rc = server_post(ch);
+    ch->ctx->dropin_ns[5] += now_ns() - t0;
     // the kernel had returned (its pending proposal undone: the caller sees the server
     // stopped and re-issues that proposal's commit): answer with a one-off launch
     if (rc == kExitedEarly) return shadow_chain_query(ch, x, y, z, edit, val);
@@ -1343,6 +1618,14 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
     const double v[8] = {(double)p.action, (double)p.active, (double)p.valid, (double)p.index, p.x, p.y, p.z, p.zeta};
     std::memcpy(out, v, sizeof v);
     return 0;
+}
+int tdt_dropin_timing(td_ctx *ctx, int reset, int64_t out[12]) {
+    if (!ctx) return TD_ERR_ARG;
+    if (out)
+        for (int k = 0; k < 12; ++k) out[k] = ctx->dropin_ns[k];
+    if (reset)
+        for (int64_t &v : ctx->dropin_ns) v = 0;
+    return TD_OK;
 }
 int tdt_rounds_force_exit(td_rounds *r, const int32_t *slots, int64_t nslots) {
     if (!r || nslots < 0 || (nslots > 0 && !slots)) return TD_ERR_ARG;

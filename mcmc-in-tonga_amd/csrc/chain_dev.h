@@ -172,7 +172,38 @@ struct RoundBox {
     RoundSlot slot[1];  // [nchains]
 };
 
+// Exchange rounds (td_rounds_exchange, chain.cpp): the resident launch runs M
+// tempering rounds with no host in the loop.  At the end of round j every
+// workgroup puts its chain's exact phi into xin and raises its flag in rdy;
+// the phis of all R replicas then arrive in xout -- from an RCCL allgather
+// that a second stream issues once workgroup 0 has seen every local flag and
+// raised `ready` (the stream waits on it: hipStreamWaitValue64), followed by a
+// stream write of `gdone`; or, on one rank, from xin itself once every
+// replica's flag is up -- no atomics, only stores and loads -- and
+// every workgroup makes the same swap decisions (chain_logic.h swap_accept)
+// and takes its chain's new temperature.  Device memory except the logs.
+struct RoundX {
+    double *xin;                        // [local] this rank's phis of the round
+    const double *xout;                 // [R] every replica's phi (== xin on one rank)
+    unsigned long long *rdy;            // [local] base + j + 1 once workgroup b's phi of round j is in xin
+    unsigned long long *ready;          // base + j + 1 once all of this rank's are (workgroup 0; signal memory)
+    const unsigned long long *gdone;    // base + j + 1 after round j's allgather (null on one rank)
+    unsigned long long ready_base, gdone_base;
+    int *lev;                           // [local][R] each workgroup's copy of every replica's level
+    const double *temps;                // [R] the ladder
+    double *log_phi;                    // [M][R] the gathered phis of every round (pinned; workgroup 0)
+    int *log_lev;                       // [M][R] the levels after every round's swaps
+    long long *log_t;                   // [M][3] workgroup 0's wall clock (100 MHz): its phi published, this
+                                        // rank's phis all in, every phi gathered
+    long long *err;                     // pinned: 1 = an exchange never came (watchdog)
+    long long rnd0;                     // the ladder's round number of round 0 (its swap parity and draws)
+    unsigned long long seed;
+    int R, local, rank, M, K;           // R = 0: not an exchange launch
+};
+constexpr long long kExchangeTicks = 1000000000;  // 10 s of the 100 MHz wall clock without an exchange: give up
+
 struct ScriptArgs {
+    const RoundX *rx;  // exchange rounds (device memory), free-running chains
     int n;
     int pin;  // >= 0: the chain runs on the workgroup that lands on this XCD (L2 kept warm across launches)
     ScriptStep step[kMaxScript];

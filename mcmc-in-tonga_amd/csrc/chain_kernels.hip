@@ -782,6 +782,99 @@ __device__ void round_wait(RoundBox *rb, int b, Shared &sh, int lane, bool publi
     }
 }
 
+// Exchange rounds (chain_dev.h RoundX), wave 0 at the end of round j with the
+// chain's exact phi: publish it, wait for every replica's phi of the round,
+// make the round's swap decisions (all of them, the same in every workgroup
+// of every rank: chain_logic.h swap_accept on the gathered vector) and take
+// this chain's new temperature (sh.rT, sh.rinv2t).  sh.srv_quit = 1 when an
+// exchange never came (x.err set).  R <= 64: lane g holds replica g.
+__device__ void round_exchange(const RoundX &x, int b, long long j, Shared &sh, int lane, double phi) {
+    const int R = x.R;
+    const unsigned long long tag = x.ready_base + (unsigned long long)j + 1ull;
+    if (b == 0 && lane == 0) x.log_t[3 * j] = (long long)wall_clock64();
+    if (lane == 0) {  // phi acknowledged before the flag (the readers load the flag, then phi)
+        mb_store(reinterpret_cast<long long *>(&x.xin[b]), __double_as_longlong(phi));
+        __builtin_amdgcn_s_waitcnt(0);
+        mb_store(reinterpret_cast<long long *>(&x.rdy[b]), (long long)tag);
+    }
+    const bool one = x.gdone == nullptr;  // one rank: xout is xin, every replica's flag is local
+    const int nflags = one ? R : x.local;
+    bool ok = true;
+    if (one || b == 0) {  // wait for the flags (lane g reads flag g)
+        const long long t0 = (long long)wall_clock64();
+        while (true) {
+            const unsigned long long f =
+                lane < nflags ? (unsigned long long)mb_load(reinterpret_cast<const long long *>(&x.rdy[lane])) : tag;
+            if (__all(f >= tag)) break;
+            if ((long long)wall_clock64() - t0 > kExchangeTicks) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (!one && ok && lane == 0)  // this rank's phis are in: the exchange stream may gather
+            mb_store(reinterpret_cast<long long *>(x.ready), (long long)tag);
+        if (b == 0 && lane == 0) x.log_t[3 * j + 1] = (long long)wall_clock64();
+    }
+    if (!one && ok) {  // the allgather of round j done (the exchange stream's write)
+        const unsigned long long want = x.gdone_base + (unsigned long long)j + 1ull;
+        const long long t0 = (long long)wall_clock64();
+        while ((unsigned long long)mb_load(reinterpret_cast<const long long *>(x.gdone)) < want) {
+            if ((long long)wall_clock64() - t0 > kExchangeTicks) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (!ok) {
+        if (lane == 0) {
+            mb_store(x.err, 1ll);
+            sh.srv_quit = 1;
+        }
+        wave_sync_lds();
+        return;
+    }
+    if (b == 0 && lane == 0) x.log_t[3 * j + 2] = (long long)wall_clock64();
+    // every replica's phi and level (system-scope loads: the gathered vector bypasses the L2s)
+    const bool in = lane < R;
+    const double ph = in ? __longlong_as_double(mb_load(reinterpret_cast<const long long *>(&x.xout[lane]))) : 0.0;
+    const int lv = in ? x.lev[b * R + lane] : lane;
+    // owner of level l (lane l): the replica at that level -- a forward permute of the levels
+    const int owner = __builtin_amdgcn_ds_permute(lv * 4, lane);
+    const unsigned long long rnd = (unsigned long long)(x.rnd0 + j);
+    const int par = (int)(rnd & 1ull);
+    // pair leaders l = par, par + 2, ... < R - 1 decide the disjoint pairs (l, l + 1)
+    const bool leader = lane >= par && ((lane - par) & 1) == 0 && lane + 1 < R;
+    const int owner_hi = __shfl(owner, (lane + 1) & 63);
+    const double pa = __shfl(ph, owner & 63), pb = __shfl(ph, owner_hi & 63);
+    bool acc = false;
+    if (leader) acc = tdchain::swap_accept(pa, pb, x.temps[lane], x.temps[lane + 1], x.seed, rnd, (uint64_t)lane);
+    // every replica: its pair (led by its level, or by the level below) and that pair's fate
+    int lead = -1;
+    if (in) {
+        if (lv >= par && ((lv - par) & 1) == 0 && lv + 1 < R) lead = lv;
+        else if (lv - 1 >= par && ((lv - 1 - par) & 1) == 0) lead = lv - 1;
+    }
+    const int acc_i = __shfl((int)acc, lead < 0 ? 0 : lead);
+    const int nl = (lead >= 0 && acc_i) ? (lv == lead ? lead + 1 : lead) : lv;
+    if (in) {
+        x.lev[b * R + lane] = nl;
+        if (b == 0) {
+            x.log_phi[j * R + lane] = ph;
+            x.log_lev[j * R + lane] = nl;
+        }
+    }
+    const int me = x.rank * x.local + b;
+    const int my_level = __shfl(nl, me);
+    if (lane == 0) {
+        const double T = x.temps[my_level];
+        sh.rT = T;
+        sh.rinv2t = 1.0 / (2.0 * T);  // = params_derived's inv_2t
+    }
+    wave_sync_lds();
+}
+
 // One array of a fused block copy: U elements per thread per round, loaded
 // into registers by load(), written by store().  Several Segs loaded before
 // any is stored keep all their loads in flight at once: the launch preamble
@@ -850,7 +943,7 @@ __device__ __attribute__((noinline)) double exact_sums(const double *term, doubl
 // that code on its path.
 // SMALL: the tiles mirrored in LDS (else in HBM, with super-tiles); RLDS: the per-ray arrays and the
 // Julia order mirrored too (the 381-ray configs, 8 waves); NTH: 512 threads, or 256 (two chains per CU)
-template <bool SMALL, bool SCRIPT, int NTH, bool RLDS = SMALL>
+template <bool SMALL, bool SCRIPT, int NTH, bool RLDS = SMALL, bool ROUNDS = false>
 __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict__ dptr, long long iters,
                                                              ScriptArgs sa) {
     constexpr bool WALK = !SMALL || kSmallWalk;  // chi^2 by the event walk
@@ -876,6 +969,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     const long long t_start = prof_on ? clock64() : 0;  // diagnostic: launch preamble / epilogue (prof[76..79])
     Mailbox *const mb = SCRIPT ? sa.mb : nullptr;  // server mode: resident, steps from the mailbox (iters ignored)
     RoundBox *const rbx = SCRIPT ? nullptr : sa.rb;  // resident tempering rounds (iters ignored)
+    // exchange rounds, swaps decided here (ROUNDS instances only: the others carry none of their registers)
+    const RoundX *const rxp = (SCRIPT || !ROUNDS) ? nullptr : sa.rx;
+    const bool xch = rxp != nullptr;
     const int bchain = sa.pin >= 0 ? 0 : (int)blockIdx.x;
     const int nscript = SCRIPT ? (mb ? 1 : sa.n) : 0;  // > 0: host-given proposals (td_evaluate), iters == nscript
 
@@ -1085,7 +1181,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     double phi_r = sh.phi;
     // wave 0: the temperature of the round (tid 0 decides with it) and the round's last iteration
     double inv2t_r = sh.rinv2t;
-    long long round_end = rbx ? sh.rK : LLONG_MAX;
+    long long round_end = rbx ? sh.rK : xch ? (long long)rxp->K : LLONG_MAX;
     int cur_r = 0;
     bool pend_r = false;    // rays in HBM: an accepted proposal's chi^2 partial sums not yet written
     bool pend_sup = false;  // rays in HBM: its super-tiles' maxima not yet refreshed
@@ -1106,7 +1202,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         }
     }
     __syncthreads();
-    for (long long it = 0; it < iters && !((mb || rbx) && sh.srv_quit); ++it) {
+    for (long long it = 0; it < iters && !((mb || rbx || xch) && sh.srv_quit); ++it) {
         if (prof_on && tid == 0) sh.t_iter = clock64();
         // rays in HBM: the previous accepted proposal's super-tile maxima (their first round of
         // loads issued here, so it overlaps the partial sums' commit below)
@@ -1714,7 +1810,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                             // a tempering round's last iteration publishes phi: decided exactly (and
                             // every sum made exact) whatever the bounds say (testing: every k-th too)
-                            if (rbx && it + 1 == round_end) bdec = 0;
+                            if ((rbx || xch) && it + 1 == round_end) bdec = 0;
                             if (d.exact_every > 0 && (it % d.exact_every) == d.exact_every - 1) bdec = 0;
                             exact = bdec == 0;
                             phi_n = Sa;  // (an estimate on a decided proposal)
@@ -2030,17 +2126,23 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         // ===== end of iteration: the next proposal (wave 0; draws refilled every 64) =====
         if (wv == 0) {
             if (prof_on && lane == 0) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
-            if (rbx && it + 1 == round_end) {  // a tempering round is done: publish phi, take the next temperature
+            if ((rbx || xch) && it + 1 == round_end) {  // a tempering round is done: publish phi, take the next temperature
                 {  // (a phase F of this iteration made every sum exact already)
                     double unused = 0.0;
                     phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, false, n, phi_r, &unused);
                     if (lane == 0) sh.phi = phi_r;
                 }
-                round_wait(rbx, bchain, sh, lane, true, phi_r);  // (lane 0 = tid 0 holds phi)
+                if (rbx) {
+                    round_wait(rbx, bchain, sh, lane, true, phi_r);  // (lane 0 = tid 0 holds phi)
+                    round_end = it + 1 + sh.rK;
+                } else {
+                    const long long Kx = rxp->K;
+                    round_exchange(*rxp, bchain, (it + 1) / Kx - 1, sh, lane, phi_r);
+                    round_end = it + 1 + Kx;
+                }
                 inv2t_r = sh.rinv2t;
-                round_end = it + 1 + sh.rK;
             }
-            if (it + 1 < iters && !((mb || rbx) && sh.srv_quit)) {
+            if (it + 1 < iters && !((mb || rbx || xch) && sh.srv_quit)) {
                 if (((it + 1) & 63) == 0 && !nscript) {
                     wave_sync_lds();
                     if (sa.pre) {
@@ -2385,7 +2487,7 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
     // More chains than CUs: one chain per CU would run them in rounds of num_cus workgroups; two
     // 4-wave chains per CU run them all at once (1.35x the 8-wave kernel's rate at 512 config-3
     // chains) -- the tiles-in-LDS kernel when it fits, else the all-in-HBM one
-    if (all_auto && num_cus > 0 && nchains > num_cus && !scripted && sa.rb == nullptr &&
+    if (all_auto && num_cus > 0 && nchains > num_cus && !scripted && sa.rb == nullptr && sa.rx == nullptr &&
         (hyb <= kLdsBudget / 2 || half <= kLdsBudget / 2)) {
         packed = true;
         tiles_ok = hyb <= kLdsBudget / 2;
@@ -2398,13 +2500,22 @@ hipError_t chain_run(const DevChain *host, const DevChain *dev, int nchains, int
                               (const void *)k_chain_run<false, false, kChainThreads>,
                               (const void *)k_chain_run<false, true, kChainThreads>,
                               (const void *)k_chain_run<false, false, kChainThreads / 2>,
-                              (const void *)k_chain_run<true, false, kChainThreads / 2, false>}) {
+                              (const void *)k_chain_run<true, false, kChainThreads / 2, false>,
+                              (const void *)k_chain_run<true, false, kChainThreads, true, true>,
+                              (const void *)k_chain_run<false, false, kChainThreads, false, true>}) {
             hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
             if (e != hipSuccess) return e;
         }
         attr_set = true;
     }
-    if (small <= kLdsBudget && !force_hbm) {
+    if (sa.rx != nullptr) {  // exchange rounds: one 8-wave chain per CU
+        if (small <= kLdsBudget && all_auto)
+            hipLaunchKernelGGL((k_chain_run<true, false, kChainThreads, true, true>), dim3(grid), dim3(kChainThreads),
+                               small, s, dev, (long long)iters, sa);
+        else
+            hipLaunchKernelGGL((k_chain_run<false, false, kChainThreads, false, true>), dim3(grid),
+                               dim3(kChainThreads), big, s, dev, (long long)iters, sa);
+    } else if (small <= kLdsBudget && !force_hbm) {
         if (scripted)
             hipLaunchKernelGGL((k_chain_run<true, true, kChainThreads>), dim3(grid), dim3(kChainThreads), small, s,
                                dev, (long long)iters, sa);

@@ -401,4 +401,28 @@ TD_HD double reject_bound(const Params &P, const Proposal &p, double phi, double
     return reject_bound_t(P, P.temperature, P.inv_2t, p, phi, czeta, zeta_killed, zetanew_death, lnN);
 }
 
+// ------------------------------------------------ parallel-tempering swap ----
+// (the reference's chains are independent, main_inversion.jl:15.)
+// Round rnd tries the level pairs (l, l+1), l = rnd mod 2, 2 + rnd mod 2, ...
+// -- disjoint, so each is decided alone: a at level l, b at l+1 swap when
+// log alpha = (phi_a - phi_b)(1/(2T_l) - 1/(2T_l+1)) >= 0 or log u < log alpha,
+// u a SplitMix64 hash of (seed, rnd, l).  The same function on the host
+// (td_swap_decide, tempering.decide_swaps) and inside the resident kernel that
+// decides the swaps itself (td_rounds_exchange): det_log, not a libm log.
+TD_HD uint64_t swap_mix64(uint64_t x) {  // SplitMix64's finaliser
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+TD_HD double swap_uniform(uint64_t seed, uint64_t rnd, uint64_t level) {
+    uint64_t x = swap_mix64(seed * 0x9E3779B97F4A7C15ull + rnd);
+    x = swap_mix64(x + level * 0xD1B54A32D192ED03ull + 1ull);
+    return ((double)(x >> 12) + 0.5) / 4503599627370496.0;  // (k + 1/2) / 2^52: in (0, 1), exact
+}
+TD_HD bool swap_accept(double phi_a, double phi_b, double t_lo, double t_hi, uint64_t seed, uint64_t rnd,
+                       uint64_t level) {
+    const double la = (phi_a - phi_b) * (1.0 / (2.0 * t_lo) - 1.0 / (2.0 * t_hi));
+    return la >= 0.0 || det_log(swap_uniform(seed, rnd, level)) < la;
+}
+
 }  // namespace tdchain

@@ -21,7 +21,7 @@ struct td_ctx {
     tdstar::Geometry g;                 // device-resident ray geometry
     std::vector<int> ray_off_host;      // CSR offsets (host copy)
     std::vector<double> hx, hy, hz;     // CSR points (host copy; chain tiles are built from it)
-    std::vector<double> sig_host;
+    std::vector<double> sig_host, tS_host;  // allSig, tS (host copies: td_evaluate's chi^2 is added on the host)
     double likelihood = 0.0;            // MCsub.jl:179 constant for sig_host
 
     // one cell set (SoA x|y|z|zeta, stride cell_stride <= cell_cap), device + pinned host staging
@@ -69,6 +69,11 @@ struct td_ctx {
     size_t draws_bytes = 0;
     tdstar::td_shadow *shadow = nullptr;  // td_evaluate's incremental path (incremental.cpp)
     int incremental = 2;                // 0 full evaluates; 1 one launch per call; 2 a resident server (tdt_set_incremental)
+    // the drop-in path's time per stage, ns (tdt_dropin_timing): [0] td_evaluate, [1] its model
+    // classification, [2] its server round trip (post -> answer), [3] td_interpolate (1 point), [4] its
+    // classification, [5] its server round trip, [6] td_evaluate calls, [7] td_interpolate calls, [8] full
+    // evaluates, [9] a DROPIN chain's modeln copies, [10] its iterations' time, [11] its iterations
+    int64_t dropin_ns[12] = {};
     // td_misfit: device copies of the last (tS, sig) given and a pinned [ptS | phi] staging area
     double *mf_dev = nullptr;           // [ptS n | tS n | sig n | terms n | phi 1]
     double *mf_host = nullptr;          // pinned [ptS n | phi 1]
@@ -107,6 +112,9 @@ double julia_sum(const double *a, int64_t n);
 double likelihood_constant(const double *sig, int64_t n);
 // td_evaluate's full path: nearest search over every point, ray sums, chi^2
 // (nearest_out nullable).  The HOST chain engine calls it directly.
+double host_chi2(const double *ptS, const double *tS, const double *sig, int64_t n);  // MCsub.jl:169-172
+// wall-clock ns (the drop-in breakdown)
+int64_t now_ns();
 int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                   int64_t ncells, double *ptS_out, double *phi_out, int32_t *nearest_out = nullptr);
 // td_evaluate's incremental path (incremental.cpp): phi and ptS only.

@@ -290,6 +290,7 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
         return TD_OK;
     };
     auto full = [&]() -> int {  // the plain evaluate; its model becomes the shadow candidate
+        ctx->dropin_ns[8] += 1;
         drop_chain(s);
         s->have_last = false;
         s->last_ptS.assign((size_t)n, 0.0);
@@ -311,6 +312,17 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
     const bool srv = ctx->incremental == 2;
     if (s->dev_pending && !(srv && shadow_server_alive(s->ch))) s->dev_pending = false;  // stopped: undone
     // which state is the new model an edit of?
+    const int64_t tc = now_ns();
+    struct Lap {  // (the classification's time, however this call leaves)
+        td_ctx *c;
+        int64_t t;
+        bool on = true;
+        void stop() {
+            if (on) c->dropin_ns[1] += now_ns() - t;
+            on = false;
+        }
+        ~Lap() { stop(); }
+    } lap{ctx, tc};
     ScriptStep e2;
     ScriptStep steps[kMaxScript];
     int nsteps = 0, decision = 0;  // decision: the fate of the device's pending proposal
@@ -359,6 +371,7 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
         if (rc) return rc;
         nsteps = 0;
     }
+    lap.stop();
     e2.decision = srv ? kDecideLater : 0;
     steps[nsteps++] = e2;
     s->ptSQ.assign((size_t)n, 0.0);
@@ -388,7 +401,9 @@ int interpolate_incremental(td_ctx *ctx, const double *x, const double *y, const
     if (!s || !s->ch || !std::isfinite(qx) || !std::isfinite(qy) || !std::isfinite(qz)) return TD_OK;
     const double *in[4] = {x, y, z, zeta};
     ScriptStep e2;
+    const int64_t tc = now_ns();
     const int rb = classify(in, M, View(s->B, nullptr), &e2);
+    ctx->dropin_ns[4] += now_ns() - tc;
     const ScriptStep *edit = nullptr;
     if (rb == 0) {
         edit = nullptr;  // the committed model

@@ -197,9 +197,9 @@ hipError_t launch_nearest_grid(const double *qx, const double *qy, const double 
                                double *best_d, double *zeta0, hipStream_t s, Timer *tm = nullptr,
                                const double *stage = nullptr);
 
-// chi^2 of a given ptS (MCsub.jl:169-172, sequential in k, exact): the fused
-// one-workgroup scan up to 2048 rays, the block-wide scan beyond.  terms: n
-// doubles of scratch; phi: one double (device).
+// chi^2 of a given ptS (MCsub.jl:169-172, sequential in k, exact): the
+// block-wide exact scan of k_chi2.  terms: n doubles of scratch; phi: one
+// double (device).
 hipError_t launch_chi2(const double *ptS, const double *tS, const double *sig, int n, double *terms, double *phi,
                        hipStream_t s);
 
@@ -208,20 +208,15 @@ hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *pre
 hipError_t test_wave_delta_sum(const double *term, const double *old, const int *chg, int cnt, double C0,
                                double *prefix, double *C_end);
 hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast);
-// Testing: phi of a caller-given ptS through the evaluate path's chi^2 code --
-// path 0: the fused last-workgroup tail (n <= 2048), 1: k_chi2 (block-wide
-// exact scan, long ray lists).  terms: n doubles of scratch.
-hipError_t test_chi2(const double *ptS, const double *tS, const double *sig, int n, int path, double *terms,
-                     double *phi, hipStream_t s);
+// Testing: phi of a caller-given ptS through k_chi2 (td_misfit's chi^2).
+hipError_t test_chi2(const double *ptS, const double *tS, const double *sig, int n, double *terms, double *phi,
+                     hipStream_t s);
 hipError_t test_block_delta(const double *term, const double *term_old, double *old, const int *chg, int k0, int n,
                             double *cprefix, double *C_end, long long *events, int *mask_ok);
 
-// ptS[i] = julia_sum_j w[j] * ((0.5*(z0[j]+z0[j+1])) / 1000) per ray (MCsub.jl:147-159).
-hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm = nullptr);
-
-// phi = sequential sum_k ((ptS-tS)^2*1.0)/sig^2 (MCsub.jl:169-172).
-// per-ray t* (launch_ray_sums) and chi^2 into *phi in one launch
-hipError_t launch_ray_sums_chi2(const Geometry &g, const double *zeta0, double *ptS, double *phi, hipStream_t s,
-                                Timer *tm = nullptr, double *host_out = nullptr);
+// ptS[i] = julia_sum_j w[j] * ((0.5*(z0[j]+z0[j+1])) / 1000) per ray (MCsub.jl:147-159);
+// host_out (nullable, device address of pinned memory): a copy of ptS for the host.
+hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm = nullptr,
+                           double *host_out = nullptr);
 
 }  // namespace tdstar

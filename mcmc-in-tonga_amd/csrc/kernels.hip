@@ -300,7 +300,8 @@ __global__ __launch_bounds__(256) void k_nn_merge(const double *__restrict__ par
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ray_sums(const int *__restrict__ ray_off, int n,
                                                   const double *__restrict__ w,
-                                                  const double *__restrict__ z0, double *__restrict__ ptS) {
+                                                  const double *__restrict__ z0, double *__restrict__ ptS,
+                                                  double *host_out) {
     __shared__ double scratch[4][96];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ray = blockIdx.x * 4 + wv;
@@ -308,84 +309,21 @@ __global__ __launch_bounds__(256) void k_ray_sums(const int *__restrict__ ray_of
     const int s0 = ray_off[ray];
     const int np = ray_off[ray + 1] - s0;
     const double r = wave_ray_sum(lane, w, PlainZeta{z0}, s0, np, scratch[wv]);
-    if (lane == 0) ptS[ray] = r;
+    if (lane == 0) {
+        ptS[ray] = r;
+        if (host_out) host_out[ray] = r;  // pinned host memory (td_evaluate: no copy back)
+    }
 }
 
 // ---------------------------------------------------------------------------
 // Stage 3: chi^2, MCsub.jl:169-172, strictly sequential in k, reproduced
-// exactly with binade-segmented integer scans (exact_sum.h).  Up to kChi2Lds
-// rays it is fused into the ray-sum launch: the last workgroup to finish its
-// rays (a device-scope counter) stages the terms in LDS and one wave sums
-// them.  Longer ray lists get a 1024-thread launch of their own (k_chi2): the
-// block-wide scan, the one-wave sum if its guess fails.
+// exactly with binade-segmented integer scans (exact_sum.h): k_chi2, a
+// 1024-thread launch (the block-wide scan, the one-wave sum if its guess
+// fails) -- td_misfit's chi^2 of gathered ray shards.  td_evaluate's ptS land
+// in pinned host memory, where the host adds the n terms in k order itself
+// (api.cpp host_chi2): shorter than any launch.
 // ---------------------------------------------------------------------------
 constexpr int kChi2Threads = 1024;
-constexpr int kChi2Lds = 2048;  // fused up to this many rays
-
-// The last workgroup's chi^2 (n <= kChi2Lds): the terms of MCsub.jl:171 in
-// LDS, then one wave adds them in k order (exact_sum.h wave_seq_sum).  Every
-// thread of the block calls it; thread 0's return value is phi.
-__device__ __forceinline__ double chi2_fused_tail(const double *ptS, const double *__restrict__ tS,
-                                                  const double *__restrict__ sig, int n, double *lterm) {
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const double d = ptS[k] - tS[k];
-        const double sg = sig[k];
-        lterm[k] = ((d * d) * 1.0) / (sg * sg);  // MCsub.jl:171
-    }
-    __syncthreads();
-    double C = 0.0;
-    if ((threadIdx.x >> 6) == 0) {
-        bool stopped = false;
-        C = wave_seq_sum(lterm, n, 0.0, nullptr, (int)(threadIdx.x & 63), nullptr, &stopped);
-    }
-    return C;
-}
-
-__global__ __launch_bounds__(256) void k_ray_sums_chi2(const int *__restrict__ ray_off, int n,
-                                                       const double *__restrict__ w,
-                                                       const double *__restrict__ z0, double *ptS,
-                                                       const double *__restrict__ tS,
-                                                       const double *__restrict__ sig, double *__restrict__ terms,
-                                                       double *__restrict__ phi, unsigned *__restrict__ done,
-                                                       double *host_out) {
-    __shared__ double scratch[4][96];
-    __shared__ double lterm[kChi2Lds];
-    __shared__ int last;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ray = blockIdx.x * 4 + wv;
-    if (ray < n) {  // wave-uniform
-        const int s0 = ray_off[ray];
-        const int np = ray_off[ray + 1] - s0;
-        const double r = wave_ray_sum(lane, w, PlainZeta{z0}, s0, np, scratch[wv]);
-        if (lane == 0) {
-            ptS[ray] = r;
-            if (host_out) host_out[1 + ray] = r;  // pinned host memory: [phi, ptS]
-        }
-    }
-    if (n > kChi2Lds) return;  // long ray lists: k_chi2 (a launch of its own) follows
-    __threadfence();  // this workgroup's ptS, device-wide, before it counts itself done
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();  // every other workgroup's ptS
-    const double C = chi2_fused_tail(ptS, tS, sig, n, lterm);
-    if (threadIdx.x == 0) {
-        *phi = C;
-        if (host_out) host_out[0] = C;
-        *done = 0u;  // ready for the next evaluation
-        __threadfence_system();
-    }
-}
-
-// The chi^2 of the fused evaluate on a caller-given ptS (testing: pins this
-// exact code to model.jld's phi values, tdt_chi2).
-__global__ __launch_bounds__(256) void k_test_chi2_fused(const double *ptS, const double *__restrict__ tS,
-                                                         const double *__restrict__ sig, int n, double *phi) {
-    __shared__ double lterm[kChi2Lds];
-    const double C = chi2_fused_tail(ptS, tS, sig, n, lterm);
-    if (threadIdx.x == 0) *phi = C;
-}
 
 __global__ __launch_bounds__(kChi2Threads) void k_chi2(const double *__restrict__ ptS,
                                                        const double *__restrict__ tS,
@@ -509,21 +447,16 @@ hipError_t test_wave_seq_sum(const double *term, int cnt, double C0, double *pre
     return hipGetLastError();
 }
 
-hipError_t test_chi2(const double *ptS, const double *tS, const double *sig, int n, int path, double *terms,
-                     double *phi, hipStream_t s) {
-    if (path == 0) {
-        if (n > kChi2Lds) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_test_chi2_fused, dim3(1), dim3(256), 0, s, ptS, tS, sig, n, phi);
-    } else {
-        hipLaunchKernelGGL(k_chi2, dim3(1), dim3(kChi2Threads), 0, s, ptS, tS, sig, n, terms, phi, nullptr);
-    }
+hipError_t test_chi2(const double *ptS, const double *tS, const double *sig, int n, double *terms, double *phi,
+                     hipStream_t s) {
+    hipLaunchKernelGGL(k_chi2, dim3(1), dim3(kChi2Threads), 0, s, ptS, tS, sig, n, terms, phi, nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_chi2(const double *ptS, const double *tS, const double *sig, int n, double *terms, double *phi,
                        hipStream_t s) {
     if (n <= 0) return hipMemsetAsync(phi, 0, sizeof(double), s);  // MCsub.jl:169 C = 0
-    return test_chi2(ptS, tS, sig, n, n <= kChi2Lds ? 0 : 1, terms, phi, s);
+    return test_chi2(ptS, tS, sig, n, terms, phi, s);
 }
 
 hipError_t test_exact_sum(const double *term, int cnt, double C0, double *prefix, double *C_end, int *fast) {
@@ -665,29 +598,13 @@ hipError_t launch_nearest(const double *qx, const double *qy, const double *qz, 
     return hipGetLastError();
 }
 
-hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm) {
+hipError_t launch_ray_sums(const Geometry &g, const double *zeta0, double *ptS, hipStream_t s, Timer *tm,
+                           double *host_out) {
     if (g.n <= 0) return hipSuccess;
     hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
     hipLaunchKernelGGL(k_ray_sums, dim3((unsigned)((g.n + 3) / 4)), dim3(256), 0, s, g.ray_off, (int)g.n, g.w,
-                       zeta0, ptS);
+                       zeta0, ptS, host_out);
     if (tm) tm->end("ray_sums", t0, s);
-    return hipGetLastError();
-}
-
-hipError_t launch_ray_sums_chi2(const Geometry &g, const double *zeta0, double *ptS, double *phi, hipStream_t s,
-                                Timer *tm, double *host_out) {
-    if (g.n <= 0) {  // no rays: chi^2 = 0 (MCsub.jl:169)
-        hipError_t e = hipMemsetAsync(phi, 0, sizeof(double), s);
-        if (e == hipSuccess && host_out) e = hipMemcpyAsync(host_out, phi, sizeof(double), hipMemcpyDeviceToHost, s);
-        return e;
-    }
-    hipEvent_t t0 = tm ? tm->begin(s) : nullptr;
-    hipLaunchKernelGGL(k_ray_sums_chi2, dim3((unsigned)((g.n + 3) / 4)), dim3(256), 0, s, g.ray_off, (int)g.n, g.w,
-                       zeta0, ptS, g.tS, g.sig, g.terms, phi, g.done, host_out);
-    if (g.n > kChi2Lds)
-        hipLaunchKernelGGL(k_chi2, dim3(1), dim3(kChi2Threads), 0, s, ptS, g.tS, g.sig, (int)g.n, g.terms, phi,
-                           host_out);
-    if (tm) tm->end("ray_sums_chi2", t0, s);
     return hipGetLastError();
 }
 

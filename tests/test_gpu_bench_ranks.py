@@ -2,8 +2,9 @@
 one process per rank), rehearsed on one GPU: two ranks over gloo, both on
 device 0 (TD_BENCH_BACKEND=gloo TD_BENCH_DEVICE=0), reduced sizes.  The
 JSON line must carry the config-4 ranks block with a swap trace equal to the
-one-process ladder's, and the config-5 stress chains block (BASELINE configs
-4 and 5; main_inversion.jl:15, define_TDstructure.jl:56)."""
+one-process ladder's, its per-round split and roofline, and the config-5
+stress chains block with its roofline (BASELINE configs 4 and 5;
+main_inversion.jl:15, define_TDstructure.jl:56)."""
 import json
 import os
 import socket
@@ -37,7 +38,13 @@ def test_bench_two_ranks_gloo():
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["roofline"]["bound"] == "latency"
     c4 = out["config4_ranks"]
     assert c4["replicas"] == 2 and c4["trace_matches_single_process"] is True, c4
-    assert c4["proposals_per_s"] > 0 and c4["allgather_us_per_round"] > 0
+    assert c4["proposals_per_s"] > 0
+    hl = c4["modes"]["host_loop"]  # (gloo: no device_swaps mode, which needs RCCL)
+    assert set(hl["split_us_per_round"]) == {"compute", "gather", "decide"} and hl["split_us_per_round"]["gather"] > 0
+    for roof in (c4["roofline"], hl["roofline"]):
+        assert roof["bound"] == "latency" and roof["achieved"] > 0 and roof["unit"] == "GB/s"
+        assert roof["latency"]["cycles_per_proposal"] > 0
     sc = out["stress_chains"]
     assert sc["chains"] == 2 and sc["proposals_per_s"] > 0
+    assert sc["roofline"]["bound"] == "latency" and sc["roofline"]["achieved"] > 0
     assert "stress_sharded" in out

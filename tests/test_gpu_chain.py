@@ -340,6 +340,88 @@ def test_resident_rounds_partial_exit(tt, ds, ctx):
         assert x["iterations"] == y["iterations"] == 24 * 10 + 60
 
 
+def test_resident_rounds_do_not_hold_back_other_streams(tt, ds, ctx):
+    """The resident rounds launch spins between rounds on a hardware queue of
+    its own (a CU-masked stream): work on other streams -- what an RCCL
+    collective's kernel is -- completes at once instead of waiting behind it
+    for the 200 ms idle watchdog, and the launch is still there for the next
+    round.  Eight ordinary HIP streams (dealt by HIP over its 4 shared
+    hardware queues) each run a fill kernel (hipMemsetAsync) while the launch
+    waits between rounds.  (Plain HIP through ctypes: the process's HIP
+    runtime is the one libtdstar loaded; torch would bring a second one.)"""
+    import time
+
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    buf = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(1 << 24)) == 0
+    streams = []
+    for _ in range(8):
+        st = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+        streams.append(st)
+    for st in streams:  # warm
+        assert hip.hipMemsetAsync(buf, 0, ctypes.c_size_t(1 << 24), st) == 0
+        assert hip.hipStreamSynchronize(st) == 0
+    prm = tt.define_TDstructrure().replace(max_cells=600)
+    chains = [make(tt, ctx, prm, tt.random_model(200 + 30 * j, 260 + j), 260 + j, tt.TD_ENGINE_DEVICE,
+                   chain=1 + j) for j in range(4)]
+    lad = tt.TemperingLadder(chains, tmax=8.0, seed=3)
+    for _ in range(5):
+        lad.step(10)
+    worst = 0.0
+    for r in range(24):
+        lad.step(10)  # the launch now waits for the next round
+        st = streams[r % len(streams)]
+        t0 = time.perf_counter()
+        assert hip.hipMemsetAsync(buf, r, ctypes.c_size_t(1 << 24), st) == 0
+        assert hip.hipStreamSynchronize(st) == 0
+        worst = max(worst, time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    for _ in range(50):
+        lad.step(10)
+    per_round = (time.perf_counter() - t0) / 50
+    lad.close()
+    for c in chains:
+        c.close()
+    for st in streams:
+        hip.hipStreamDestroy(st)
+    hip.hipFree(buf)
+    assert worst < 0.05, worst  # (held back: >= 0.2 s, the watchdog)
+    assert per_round < 0.02, per_round
+
+
+@pytest.mark.parametrize("lds_mode", [0, 1])
+def test_exchange_rounds_equal_host_decided(tt, ds, ctx, lds_mode):
+    """td_rounds_exchange on one rank (the swaps decided inside the kernel,
+    no host in the loop) against the host-decided resident ladder, in both
+    layouts (lds_mode 1: the HBM-layout kernel) and two calls of different
+    round sizes; then the chains alone, each at its final level's T."""
+    prm = tt.define_TDstructrure().replace(max_cells=600)
+    runs = []
+    for dev_swaps in (True, False):
+        chains = [make(tt, ctx, prm, tt.random_model(220 + 25 * j, 300 + j), 300 + j, tt.TD_ENGINE_DEVICE,
+                       chain=1 + j) for j in range(5)]
+        for c in chains:
+            assert tt.lib().tdt_chain_set_lds_mode(c.h, lds_mode) == 0
+        lad = tt.TemperingLadder(chains, tmax=6.0, seed=31, device_swaps=dev_swaps)
+        assert lad.device_swaps == dev_swaps
+        lad.run(30, 10)
+        lad.run(13, 3)
+        lad.close()
+        for c in chains:
+            c.run(40)
+        runs.append((lad.trace_digest(), list(lad.levels), list(lad.tried), list(lad.accepted), lad.mixing(),
+                     [c.model() for c in chains], [c.stats() for c in chains]))
+        for c in chains:
+            c.close()
+    a, b = runs
+    assert a[:5] == b[:5]
+    assert sum(a[3]) > 0  # swaps happened
+    for ma, mb, x, y in zip(a[5], b[5], a[6], b[6]):
+        assert same_models(ma, mb)
+        assert x["phi"] == y["phi"] and x["accepted"] == y["accepted"] and x["iterations"] == y["iterations"]
+
+
 def test_library_tempering_loop_equals_round_by_round(tt, ds, ctx):
     """TemperingLadder.run (td_rounds_temper: the resident launch with the swap
     steps decided in the library between rounds, no return to Python per

@@ -6,8 +6,9 @@ geometry is not shipped, so the nearest search cannot be replayed; but every
 device code path that turns a ptS into phi (MCsub.jl:169-172) can be fed the
 reference's ptS and must return the reference's phi bit for bit:
 
-  path 0  td_evaluate's fused chi^2 (last workgroup, one-wave exact scan)
-  path 1  td_evaluate's block-wide exact scan (long ray lists)
+  path 0  td_evaluate's chi^2 (the host adds the terms in k order where the
+          ray-sum kernel put ptS)
+  path 1  td_misfit's block-wide exact scan (k_chi2)
   path 2  the device chain's starting-state prefix sums (k_chi2_prefix)
   path 3  the device chain's proposal-time scan, from k0 = 0 and restarted
           at k0 = n/2 on path 2's prefix

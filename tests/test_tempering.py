@@ -171,9 +171,12 @@ def test_native_swap_step_is_decide_swaps(tt):
                             ctypes.c_uint64(1), out.ctypes.data_as(P64), None, None) != 0
 
 
-def test_resident_rounds_not_under_a_gpu_collective():
-    """Resident rounds (one spinning launch) only when the gather is not an RCCL
-    collective: with few hardware queues the collective could wait behind it."""
+def test_resident_rounds_under_a_gpu_collective():
+    """Resident rounds (one spinning launch) also when the gather is an RCCL
+    collective: the launch has a hardware queue of its own (a CU-masked
+    stream), so the collective's kernels are not held back behind it
+    (tests/test_gpu_chain.py::test_resident_rounds_do_not_hold_back_other_streams).
+    Device swaps need one rank or the library's communicator."""
 
     class DeviceStandIn(ToyChain):
         h, ctx = 1, "ctx"
@@ -194,8 +197,12 @@ def test_resident_rounds_not_under_a_gpu_collective():
     chains = [DeviceStandIn(1), DeviceStandIn(2)]
     assert tempering.TemperingLadder(chains).resident
     assert tempering.TemperingLadder(chains, exchange=tempering.Exchange(FakeDist(2), "cpu")).resident
-    assert not tempering.TemperingLadder(chains, exchange=tempering.Exchange(FakeDist(2), "cuda:0")).resident
+    assert tempering.TemperingLadder(chains, exchange=tempering.Exchange(FakeDist(2), "cuda:0")).resident
     assert not tempering.TemperingLadder(chains, resident=False).resident
+    assert tempering.TemperingLadder(chains, device_swaps=True).device_swaps
+    assert not tempering.TemperingLadder(chains, exchange=tempering.Exchange(FakeDist(2), "cuda:0"),
+                                         device_swaps=True).device_swaps  # (no communicator)
+    assert not tempering.TemperingLadder(chains, resident=False, device_swaps=True).device_swaps
 
 
 def test_round_trip_counting():

@@ -7,3 +7,6 @@ tail -3 $out/tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { echo smoke failed; cat $out/smoke.log; exit 1; }
 timeout -k 10 600 python bench.py > $out/bench.log 2>&1 || { echo bench failed; tail $out/bench.log; exit 1; }
 cat $out/smoke.log; tail -1 $out/bench.log | cut -c1-600
+# the ladder calibration sweep (config-4 shape, device-decided rounds)
+timeout -k 10 300 python tools/calibrate_ladder.py $out/calib.json 2000 200 > $out/calib.log 2>&1 || { echo calib failed; tail $out/calib.log; exit 1; }
+cut -c1-300 $out/calib.log
