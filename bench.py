@@ -391,7 +391,32 @@ def tempering_config4(tt, ctx, ds, nrep=8, ncells=2000, swap_every=10, rounds=30
         if comm is not None:
             comm.close()
     res["modes_same_trace"] = len(digests) == 1
+    res["calibrated"] = calibrated_ladder(tt, ctx, ds, nrep, ncells, swap_every)
     return res
+
+
+def calibrated_ladder(tt, ctx, ds, nrep=8, ncells=2000, swap_every=10, tmax=1.1, burn=200, rounds=2000):
+    """Beside BASELINE's ladder (T in [1, 8]: its replicas' misfits differ by
+    thousands, so neighbours almost never swap), the same 8 replicas on a
+    ladder that mixes at this model size: T_max = 1.1, chosen from the sweep in
+    profiles/r04/ladder_calibration.json (tools/calibrate_ladder.py) as the
+    widest ladder with every adjacent swap rate well above 20 % and replicas
+    completing round trips.  Device-decided rounds; a burn-in, then the
+    measured rounds."""
+    chains = config4_replicas(tt, ctx, ds, 0, nrep, ncells)
+    lad = tt.TemperingLadder(chains, tmax=tmax, seed=4242, device_swaps=True)
+    lad.run(burn, swap_every)
+    tried0, acc0, trips0 = lad.tried.copy(), lad.accepted.copy(), int(lad.trips.sum())
+    t0 = time.perf_counter()
+    lad.run(rounds, swap_every)
+    el = time.perf_counter() - t0
+    lad.close()
+    rates = [float(a) / t if t else 0.0 for a, t in zip(lad.accepted - acc0, lad.tried - tried0)]
+    for c in chains:
+        c.close()
+    return {"tmax": tmax, "temps": [round(t, 4) for t in lad.temps], "burn_rounds": burn, "rounds": rounds,
+            "ms_per_round": round(el / rounds * 1e3, 4), "swap_rates": [round(r, 3) for r in rates],
+            "round_trips": int(lad.trips.sum()) - trips0, "mixing": lad.mixing()}
 
 
 def exchange_cost(tt, ctx, ds, swap_every=10, rounds=300, ncells=2000):
@@ -604,7 +629,7 @@ def dropin(tt, ds, model, iters=1500, host_iters=300):
         ch.run(50)
         e0 = ch.stats()["evaluations"]
         ctx.timing(enable=True, reset=True)
-        dt = np.zeros(12, dtype=np.int64)
+        dt = np.zeros(18, dtype=np.int64)
         tt.lib().tdt_dropin_timing(ctx.h, 1, dt.ctypes.data_as(tt._lib._pi64))
         t0 = time.perf_counter()
         ch.run(k)
@@ -624,6 +649,7 @@ def dropin(tt, ds, model, iters=1500, host_iters=300):
                 "td_interpolate_1pt": us(ip), "interpolate_classify": us(dt[4]),
                 "interpolate_server_round_trip": us(dt[5]), "interpolate_rest": us(ip - dt[4] - dt[5]),
                 "host_loop_modeln_copy": us(dt[9]), "host_loop_rest": us(dt[10] - ev - ip - dt[9]),
+                "server_busy_evaluate": us(dt[16]), "server_busy_interpolate": us(dt[17]),
                 "calls_per_proposal": {"td_evaluate": round(float(dt[6]) / k, 3),
                                        "td_interpolate": round(float(dt[7]) / k, 3),
                                        "full_evaluates": int(dt[8])}}
@@ -643,8 +669,8 @@ def full_evaluate(tt, ctx, model, N, reps=50):
     cells = model.cells()
     E = ctx.P * N
     out = {}
-    kernels = {"grid": ["nn_grid_build", "nn_grid", "ray_sums_chi2"],
-               "brute_force": ["nn_tile", "nn_partial", "nn_merge", "ray_sums_chi2"]}
+    kernels = {"grid": ["nn_grid_build", "nn_grid", "ray_sums"],
+               "brute_force": ["nn_tile", "nn_partial", "nn_merge", "ray_sums"]}
     tt.lib().tdt_set_incremental(ctx.h, 0)  # every call a full evaluate (repeats would hit the shadow's cache)
     for name, method in (("grid", ctx.NN_GRID), ("brute_force", ctx.NN_BRUTE)):
         ctx.set_nn_method(method)
@@ -654,6 +680,13 @@ def full_evaluate(tt, ctx, model, N, reps=50):
         for _ in range(reps):
             ctx.evaluate(cells)
         el = (time.perf_counter() - t0) / reps
+        dt = np.zeros(18, dtype=np.int64)
+        tt.lib().tdt_dropin_timing(ctx.h, 1, dt.ctypes.data_as(tt._lib._pi64))
+        for _ in range(reps):
+            ctx.evaluate(cells)
+        tt.lib().tdt_dropin_timing(ctx.h, 1, dt.ctypes.data_as(tt._lib._pi64))
+        host = {k: round(float(dt[i]) / 1e3 / reps, 3) for k, i in (("pack_cells", 12), ("issue_kernels", 13),
+                                                                    ("wait_kernels", 14), ("chi2_copy_out", 15))}
         ctx.timing(enable=True, reset=True)  # then the kernels, timed with HIP events
         for _ in range(reps):
             ctx.evaluate(cells)
@@ -664,7 +697,7 @@ def full_evaluate(tt, ctx, model, N, reps=50):
                 km[k] = round(ms / nl, 4)
         ctx.timing(enable=False)
         out[name] = {"evaluate_ms": round(el * 1e3, 4), "evaluates_per_s": round(1.0 / el, 1),
-                     "nn_pair_evals_per_s_equiv": round(E / el, 1), "kernel_ms": km}
+                     "nn_pair_evals_per_s_equiv": round(E / el, 1), "kernel_ms": km, "host_us": host}
     ctx.set_nn_method(ctx.NN_AUTO)
     tt.lib().tdt_set_incremental(ctx.h, 1)
     # the dominant kernel: the one-launch tile search (the split search only when forced)

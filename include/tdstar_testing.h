@@ -78,8 +78,11 @@ int tdt_rounds_force_exit(td_rounds *r, const int32_t *slots, int64_t nslots);
  * point, [4] its classification, [5] its server round trip, [6] td_evaluate
  * calls, [7] 1-point td_interpolate calls, [8] full evaluates, [9] a DROPIN
  * chain's modeln copies (the host loop's deepcopy), [10] its iterations'
- * time, [11] its iterations. */
-int tdt_dropin_timing(td_ctx *ctx, int reset, int64_t out[12]);
+ * time, [11] its iterations; the full evaluate's host side: [12] cells
+ * packed into pinned memory, [13] kernels issued, [14] the wait for them,
+ * [15] chi^2 and copy-out; [16] the resident server's busy time by its own
+ * clock (command seen -> answered), evaluate commands, [17] queries. */
+int tdt_dropin_timing(td_ctx *ctx, int reset, int64_t out[18]);
 /* The block-wide exact sequential sum (exact_sum.h, used for chi^2 over long
  * ray lists): prefix[k] = C0 + term[0] + ... + term[k] added strictly left to
  * right in FP64 (MCsub.jl:170-172).  *fast = 1 when the parallel path proved

@@ -2,8 +2,11 @@
 // interpolate.  Host-side glue only; the arithmetic is in kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <immintrin.h>
+
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -141,6 +144,57 @@ bool uses_grid(const td_ctx *ctx, int64_t ncells) {
     return ncells > 0 && (ctx->nn_method == 2 || (ctx->nn_method == 0 && ncells >= kGridMinCells));
 }
 
+// dst[0..n) = src, and the extent of src with NaN skipped (lo = v < lo ? v : lo): the staging of one
+// coordinate of the cells and the box the bucket grid is built on, in one pass.  AVX2 when the host
+// has it: minpd/maxpd return their second operand unless the first is strictly below/above, which is
+// exactly that rule (NaN and +-0 included); the 8 running extents are folded by the same rule.
+__attribute__((target("avx2"))) void copy_extent_avx2(const double *src, double *dst, int64_t n, double *lo_out,
+                                                      double *hi_out) {
+    __m256d l0 = _mm256_set1_pd(HUGE_VAL), l1 = l0, h0 = _mm256_set1_pd(-HUGE_VAL), h1 = h0;
+    int64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const __m256d a = _mm256_loadu_pd(src + i), b = _mm256_loadu_pd(src + i + 4);
+        _mm256_storeu_pd(dst + i, a);
+        _mm256_storeu_pd(dst + i + 4, b);
+        l0 = _mm256_min_pd(a, l0);
+        l1 = _mm256_min_pd(b, l1);
+        h0 = _mm256_max_pd(a, h0);
+        h1 = _mm256_max_pd(b, h1);
+    }
+    double L[8], H[8];
+    _mm256_storeu_pd(L, l0);
+    _mm256_storeu_pd(L + 4, l1);
+    _mm256_storeu_pd(H, h0);
+    _mm256_storeu_pd(H + 4, h1);
+    double lo = L[0], hi = H[0];
+    for (int k = 1; k < 8; ++k) {
+        lo = L[k] < lo ? L[k] : lo;
+        hi = H[k] > hi ? H[k] : hi;
+    }
+    for (; i < n; ++i) {
+        const double v = src[i];
+        dst[i] = v;
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    *lo_out = lo;
+    *hi_out = hi;
+}
+
+void copy_extent(const double *src, double *dst, int64_t n, double *lo_out, double *hi_out) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) return copy_extent_avx2(src, dst, n, lo_out, hi_out);
+    double lo = HUGE_VAL, hi = -HUGE_VAL;
+    for (int64_t i = 0; i < n; ++i) {
+        const double v = src[i];
+        dst[i] = v;
+        lo = v < lo ? v : lo;  // NaN compares false: skipped
+        hi = v > hi ? v : hi;
+    }
+    *lo_out = lo;
+    *hi_out = hi;
+}
+
 int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                  int64_t ncells) {
     int rc = ensure_cells(ctx, ncells);
@@ -152,14 +206,8 @@ int upload_cells(td_ctx *ctx, const double *x, const double *y, const double *z,
     double *h = ctx->h_cells;
     const double *src[3] = {x, y, z};
     for (int a = 0; a < 3; ++a) {  // staged, and the box of the cells for the bucket grid, in one pass
-        double lo = HUGE_VAL, hi = -HUGE_VAL;
-        double *dst = h + a * s;
-        for (int64_t i = 0; i < ncells; ++i) {
-            const double v = src[a][i];
-            dst[i] = v;
-            lo = v < lo ? v : lo;  // NaN compares false: skipped
-            hi = v > hi ? v : hi;
-        }
+        double lo, hi;
+        copy_extent(src[a], h + a * s, ncells, &lo, &hi);
         ctx->cell_lo[a] = lo <= hi ? lo : 0.0;
         ctx->cell_hi[a] = lo <= hi ? hi : 0.0;
     }
@@ -207,8 +255,10 @@ double host_chi2(const double *ptS, const double *tS, const double *sig, int64_t
 
 int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                   int64_t ncells, double *ptS_out, double *phi_out, int32_t *nearest_out) {
+    const int64_t t0 = now_ns();
     int rc = upload_cells(ctx, x, y, z, zeta, ncells);
     if (rc) return rc;
+    const int64_t t1 = now_ns();
     const auto &g = ctx->g;
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
     hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, ncells, ctx->best_i, ctx->best_d, ctx->zeta0);
@@ -219,11 +269,18 @@ int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z
     if (nearest_out && g.P)
         TD_HIP(ctx, hipMemcpyAsync(ctx->h_best_i, ctx->best_i, sizeof(int) * (size_t)g.P, hipMemcpyDeviceToHost,
                                    ctx->stream));
+    const int64_t t2 = now_ns();
     TD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const int64_t t3 = now_ns();
     // chi^2: the n terms added in k order by the host, where ptS already is (MCsub.jl:169-172)
     const double phi = host_chi2(ctx->h_out + 1, ctx->tS_host.data(), ctx->sig_host.data(), g.n);
     if (phi_out) *phi_out = phi;
     if (ptS_out && g.n) std::memcpy(ptS_out, ctx->h_out + 1, sizeof(double) * (size_t)g.n);
+    const int64_t t4 = now_ns();
+    ctx->dropin_ns[12] += t1 - t0;
+    ctx->dropin_ns[13] += t2 - t1;
+    ctx->dropin_ns[14] += t3 - t2;
+    ctx->dropin_ns[15] += t4 - t3;
     if (nearest_out && g.P) std::memcpy(nearest_out, ctx->h_best_i, sizeof(int) * (size_t)g.P);
     return TD_OK;
 }
@@ -239,7 +296,7 @@ void free_ctx(td_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     shadow_free(c);
     c->timer.release();
-    void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->g.done, c->cells,
+    void *dev[] = {c->g.px, c->g.py, c->g.pz, c->g.w, c->g.ray_off, c->g.tS, c->g.sig, c->g.terms, c->cells,
                    c->nn.part_d, c->nn.part_i, c->best_i, c->best_d, c->zeta0, c->phi,
                    c->q, c->q_i, c->q_z, c->chain_desc, c->draws, c->nn.g_count, c->nn.g_ent, c->raster, c->raster_i, c->raster_off,
                    c->mf_dev};
@@ -332,6 +389,7 @@ int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, 
     c->g.n = n;
     c->g.P = P;
     c->ray_off_host = off;
+
     c->hx = hx;
     c->hy = hy;
     c->hz = hz;
@@ -354,8 +412,6 @@ int td_create(td_ctx **out, int device, const double *rayX, const double *rayY, 
     rc = rc ? rc : dalloc((void **)&c->g.tS, nb, "hipMalloc(tS)");
     rc = rc ? rc : dalloc((void **)&c->g.sig, nb, "hipMalloc(sig)");
     rc = rc ? rc : dalloc((void **)&c->g.terms, nb, "hipMalloc(terms)");
-    rc = rc ? rc : dalloc((void **)&c->g.done, sizeof(unsigned), "hipMalloc(done)");
-    if (!rc && hipMemset(c->g.done, 0, sizeof(unsigned)) != hipSuccess) rc = hip_err(c, hipErrorUnknown, "hipMemset(done)");
     rc = rc ? rc : dalloc((void **)&c->best_i, sizeof(int) * (size_t)(P > 0 ? P : 1), "hipMalloc(best_i)");
     rc = rc ? rc : dalloc((void **)&c->best_d, Pb, "hipMalloc(best_d)");
     rc = rc ? rc : dalloc((void **)&c->zeta0, Pb, "hipMalloc(zeta0)");

@@ -1529,6 +1529,7 @@ int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int 
         const int64_t t0 = now_ns();
         rc = server_post(ch);
         ch->ctx->dropin_ns[2] += now_ns() - t0;
+        if (rc == TD_OK) ch->ctx->dropin_ns[16] += 10 * *vol(&ch->mb_host->diag[1]);  // (100 MHz ticks)
         if (rc == TD_OK) {
             ch->srv_pending = st[nsteps - 1];
             ch->srv_has_pending = st[nsteps - 1].decision == kDecideLater;
@@ -1567,6 +1568,7 @@ int shadow_server_query(td_chain *ch, double x, double y, double z, const Script
     const int64_t t0 = now_ns();
     rc = server_post(ch);
     ch->ctx->dropin_ns[5] += now_ns() - t0;
+    if (rc == TD_OK) ch->ctx->dropin_ns[17] += 10 * *vol(&ch->mb_host->diag[1]);
     // the kernel had returned (its pending proposal undone: the caller sees the server
     // stopped and re-issues that proposal's commit): answer with a one-off launch
     if (rc == kExitedEarly) return shadow_chain_query(ch, x, y, z, edit, val);
@@ -1619,10 +1621,10 @@ int tdt_propose(const td_chain_params *prm, uint64_t iter, int64_t ncells, const
     std::memcpy(out, v, sizeof v);
     return 0;
 }
-int tdt_dropin_timing(td_ctx *ctx, int reset, int64_t out[12]) {
+int tdt_dropin_timing(td_ctx *ctx, int reset, int64_t out[18]) {
     if (!ctx) return TD_ERR_ARG;
     if (out)
-        for (int k = 0; k < 12; ++k) out[k] = ctx->dropin_ns[k];
+        for (int k = 0; k < 18; ++k) out[k] = ctx->dropin_ns[k];
     if (reset)
         for (int64_t &v : ctx->dropin_ns) v = 0;
     return TD_OK;

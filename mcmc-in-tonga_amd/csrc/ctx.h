@@ -72,8 +72,11 @@ struct td_ctx {
     // the drop-in path's time per stage, ns (tdt_dropin_timing): [0] td_evaluate, [1] its model
     // classification, [2] its server round trip (post -> answer), [3] td_interpolate (1 point), [4] its
     // classification, [5] its server round trip, [6] td_evaluate calls, [7] td_interpolate calls, [8] full
-    // evaluates, [9] a DROPIN chain's modeln copies, [10] its iterations' time, [11] its iterations
-    int64_t dropin_ns[12] = {};
+    // evaluates, [9] a DROPIN chain's modeln copies, [10] its iterations' time, [11] its iterations;
+    // the full evaluate's host side: [12] cells packed into pinned memory, [13] kernels issued, [14] the
+    // wait for them, [15] chi^2 and copy-out; [16] server busy, ns (the kernel's own clock), evaluate
+    // commands, [17] the same, queries
+    int64_t dropin_ns[18] = {};
     // td_misfit: device copies of the last (tS, sig) given and a pinned [ptS | phi] staging area
     double *mf_dev = nullptr;           // [ptS n | tS n | sig n | terms n | phi 1]
     double *mf_host = nullptr;          // pinned [ptS n | phi 1]

@@ -155,7 +155,6 @@ struct Geometry {
     int *ray_off = nullptr;
     double *tS = nullptr, *sig = nullptr;
     double *terms = nullptr;  // [n] scratch: chi^2 terms of one evaluation
-    unsigned *done = nullptr;  // workgroups of the ray-sum launch that finished (0 between launches)
 };
 
 // How a cell set is split over workgroups for the brute-force search.

@@ -105,6 +105,30 @@ def test_edge_rays_and_long_rays(tt, orc):
     c2.close()
 
 
+def test_long_and_short_rays_on_the_grid(tt, orc):
+    """Rays of 1, 2, 9, 17 and 2100 points (Julia's pairwise split above 1024
+    terms) through the grid search (>= 256 cells) against the oracle."""
+    m = 2100
+    t = np.linspace(0, 1, m)[:, None]
+    rays = [np.array([[1.0, 2.0, 3.0]]), np.array([[0, 0, 0], [10, 0, 5.0]]),
+            np.array([300.0, 50.0, 100.0]) + np.linspace(0, 1, 9)[:, None] * np.array([50.0, 20.0, 30.0]),
+            np.array([500.0, -50.0, 200.0]) + np.linspace(0, 1, 17)[:, None] * np.array([-80.0, 40.0, 60.0]),
+            np.array([20.0, -100.0, 600.0]) + t * np.array([800.0, 300.0, -600.0])]
+    n = len(rays)
+    X, Y, Z = (np.full((m, n), np.nan) for _ in range(3))
+    for i, r in enumerate(rays):
+        X[:len(r), i], Y[:len(r), i], Z[:len(r), i] = r[:, 0], r[:, 1], r[:, 2]
+    U = np.where(np.isnan(X), np.nan, 0.1 + 0.001 * np.nan_to_num(Z))
+    L, Uu = tt.segments(X, Y, Z, U)
+    tS = np.linspace(0.1, 0.5, n)
+    sig = np.linspace(0.05, 0.3, n)
+    ds2 = tt.DataStruct(tS, tS, tS, tS, sig, tS, tS, tS, tS, tS, tS, tS, tS, tS, tS, tS, tS, X, Y, Z, L, Uu, U)
+    c2 = tt.TdContext.from_datastruct(ds2)
+    for nc, seed in ((300, 4), (2000, 5)):
+        assert_same(c2, orc, ds2, tt.random_model(nc, seed).cells())
+    c2.close()
+
+
 def test_layout_error_is_reported(tt, ds):
     L = ds.rayL.copy()
     L[3, 10] = np.nan
