@@ -14,12 +14,13 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from summarize import counters, mean, trace_rows  # noqa: E402
 
 ROWS = {  # traffic.json key -> (run, kernel name)
-    "k_chain_run/single": ("single", "k_chain_run<true, false, 512, true>"),
-    "k_chain_run/many256": ("many", "k_chain_run<true, false, 512, true>"),
-    "k_chain_run/many512x2": ("packed", "k_chain_run<true, false, 256, false>"),
+    "k_chain_run/single": ("single", "k_chain_run<true, false, 512, true, false>"),
+    "k_chain_run/many256": ("many", "k_chain_run<true, false, 512, true, false>"),
+    "k_chain_run/many512x2": ("packed", "k_chain_run<true, false, 256, false, false>"),
     "k_nn_tile/config3": ("single", "k_nn_tile<2>"),
     "k_nn_grid/config3": ("single", "k_nn_grid"),
-    "k_chain_run/stress": ("stress", "k_chain_run<false, false, 512, false>"),
+    "k_chain_run/stress": ("stress", "k_chain_run<false, false, 512, false, false>"),
+    "k_chain_run/exchange": ("config4", "k_chain_run<true, false, 512, true, true>"),
     "k_nn_grid4/stress": ("stress", "k_nn_grid4"),
     "k_nn_tile/stress": ("stress", "k_nn_tile<2>"),
     "k_raster_brute/section": ("aux", "k_raster_brute"),
@@ -27,7 +28,11 @@ ROWS = {  # traffic.json key -> (run, kernel name)
 
 
 def main(d, tag):
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "traffic.json")
     out = {}
+    if os.path.exists(path):  # rows this run has no PMC passes for keep their earlier source
+        with open(path) as f:
+            out = json.load(f)
     for key, (run, kern) in ROWS.items():
         agg = counters(os.path.join(d, run), True)
         v = agg.get(kern)
@@ -43,7 +48,6 @@ def main(d, tag):
                     "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B); "
                             "KB = 1024 B; dominant dispatches (>= 1/2 the longest) only",
                     "source": "profiles/%s_%s.md" % (tag, run)}
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "traffic.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
