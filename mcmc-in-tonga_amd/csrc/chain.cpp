@@ -316,6 +316,28 @@ int device_setup(td_chain *ch) {
         }
         std::stable_sort(torder.begin(), torder.end(), [&](int a, int b) { return key[(size_t)a] < key[(size_t)b]; });
     }
+    {
+        // The LDS layout's tile pass gives each wave runs of 64 consecutive tiles, and a wave
+        // preloads the points of only the first kPre tiles it finds (phase B).  The tiles one
+        // proposal hits are Morton neighbours: dealt round-robin over the 8 waves instead
+        // (Morton rank J*512 + r -> J*512 + (r % 8) * 64 + r / 8, whole rounds of 512), each wave
+        // finds one or two and phase C reads no point of its own.  The HBM layout keeps the
+        // Morton order: its super-tiles are 16 consecutive tiles.
+        DevChain probe{};
+        probe.ntiles = ntiles;
+        probe.n = (int)n;
+        probe.cap = std::max<int>(ch->prm.max_cells, (int)ch->x.size()) + 1;
+        int64_t sz[4];
+        chain_lds_sizes(probe, sz);
+        if (sz[0] <= 160 * 1024) {
+            constexpr int kRound = kChainThreads, kW = kChainThreads / 64;
+            std::vector<int> dealt(torder);
+            for (int J = 0; (J + 1) * kRound <= ntiles; ++J)
+                for (int r = 0; r < kRound; ++r)
+                    dealt[(size_t)J * kRound + (size_t)(r % kW) * 64 + (size_t)(r / kW)] = torder[(size_t)J * kRound + r];
+            torder.swap(dealt);
+        }
+    }
     std::vector<int> tsc((size_t)ntiles + 1, 0), tray2((size_t)ntiles);
     std::vector<float> lo2(lo.size()), hi2(hi.size());
     for (int i = 0; i < ntiles; ++i) {
