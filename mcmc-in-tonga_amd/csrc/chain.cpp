@@ -367,12 +367,15 @@ int device_setup(td_chain *ch) {
     const CellGrid G = make_cell_grid(glo, ghi, std::max<double>((double)ch->x.size(), 16.0) / 2.0, 256, 1 << 24);
     const size_t nbuckets = (size_t)G.gx * G.gy * G.gz;
     std::vector<int> bcount(nbuckets, 0);
-    std::vector<BucketEntry> bent(nbuckets * kBucketCap, BucketEntry{0.0, 0.0, 0.0, 0, 0});
+    std::vector<CellEntry> bent(nbuckets * kBucketCap, CellEntry{0.0, 0.0, 0.0, 0.0});
+    std::vector<int> bslot(nbuckets * kBucketCap, 0);
     int overflow = 0;
     for (size_t i = 0; i < ch->x.size(); ++i) {
         const int b = grid_bucket(G, ch->x[i], ch->y[i], ch->z[i]);
-        if (bcount[(size_t)b] < kBucketCap)
-            bent[(size_t)b * kBucketCap + bcount[(size_t)b]++] = BucketEntry{ch->x[i], ch->y[i], ch->z[i], (int)i, 0};
+        if (bcount[(size_t)b] < kBucketCap) {
+            bslot[(size_t)b * kBucketCap + bcount[(size_t)b]] = (int)i;
+            bent[(size_t)b * kBucketCap + bcount[(size_t)b]++] = CellEntry{ch->x[i], ch->y[i], ch->z[i], ch->zeta[i]};
+        }
         else
             overflow = 1;
     }
@@ -389,7 +392,7 @@ int device_setup(td_chain *ch) {
     add(sizeof(int) * Pn); add(sizeof(int) * Pn); add(sizeof(int) * (ntiles + 1));
     for (int i = 0; i < 6; ++i) add(sizeof(double) * nn);
     add(sizeof(int) * nn); add(sizeof(int) * nn); add(sizeof(ChainScalars));
-    add(sizeof(int) * nbuckets); add(sizeof(BucketEntry) * nbuckets * kBucketCap); add(sizeof(int));
+    add(sizeof(int) * nbuckets); add(sizeof(CellEntry) * nbuckets * kBucketCap); add(sizeof(int) * nbuckets * kBucketCap); add(sizeof(int));
     add(sizeof(DevChain));
     hipError_t e = hipMalloc(&ch->dev_block, bytes);
     if (e != hipSuccess) return hip_err(c, e, "hipMalloc(chain state)");
@@ -431,7 +434,8 @@ int device_setup(td_chain *ch) {
     d.st = carve<ChainScalars>(cur, 1);
     d.grid = G;
     d.bucket_count = carve<int>(cur, nbuckets);
-    d.buckets = carve<BucketEntry>(cur, nbuckets * kBucketCap);
+    d.buckets = carve<CellEntry>(cur, nbuckets * kBucketCap);
+    d.bslot = carve<int>(cur, nbuckets * kBucketCap);
     d.grid_overflow = carve<int>(cur, 1);
     ch->dev_ptr = carve<DevChain>(cur, 1);
     ch->st_dev = d.st;
@@ -475,7 +479,8 @@ int device_setup(td_chain *ch) {
         {d.order, ident.data(), sizeof(int) * (size_t)cap},
         {d.rank, rank0.data(), sizeof(int) * (size_t)cap},
         {d.bucket_count, bcount.data(), sizeof(int) * nbuckets},
-        {d.buckets, bent.data(), sizeof(BucketEntry) * bent.size()},
+        {d.buckets, bent.data(), sizeof(CellEntry) * bent.size()},
+        {d.bslot, bslot.data(), sizeof(int) * bslot.size()},
         {d.grid_overflow, &overflow, sizeof(int)},
         {d.st, &s0, sizeof s0}};
     for (auto &u : ups)

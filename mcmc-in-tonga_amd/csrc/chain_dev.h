@@ -30,6 +30,11 @@ constexpr int kTilePts = 16;
 constexpr int kProfSlots = 80;
 constexpr int kChainThreads = 512;  // 8 waves: 256 VGPRs per lane, no spills
 constexpr int kBucketCap = 32;
+// A bucket entry of the chain's grid: the cell's site and value (its slot in a parallel array), so a
+// query's one round of loads brings the value of whichever cell wins.
+struct CellEntry {
+    double x, y, z, zeta;
+};
 
 struct ChainScalars {
     int64_t iter;          // next iteration index
@@ -110,7 +115,8 @@ struct DevChain {
     // uniform bucket grid over the cells
     CellGrid grid;
     int *bucket_count;      // [G]
-    BucketEntry *buckets;   // [G * kBucketCap]
+    CellEntry *buckets;     // [G * kBucketCap] a cell's site and value, inline: a grid search reads no cell array
+    int *bslot;             // [G * kBucketCap] the entry's slot
     int *grid_overflow;     // sticky: a bucket overflowed -> always scan all cells
 };
 

@@ -211,10 +211,12 @@ struct Shared {
     int n_super[2];  // rays in HBM: super-tiles hit, by iteration parity (the next iteration refreshes their maxima)
     int pts_seen, ray_pts;
     // bucket-grid update of an accepted proposal (applied by the last wave in phase G)
-    int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site
+    int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site, bit 4: new value in place
     // what the update needs from the grid, read during phase F (G only writes)
     int gp_bo, gp_co, gp_pos, gp_bn, gp_cn;
-    BucketEntry gp_last;
+    CellEntry gp_last;
+    int gp_last_slot;
+    double g_nzeta;
     double g_ox, g_oy, g_oz, g_nx, g_ny, g_nz;
     // chain scalars, resident for the whole launch
     long long iter, evaluations, bytes;
@@ -434,7 +436,8 @@ __device__ __attribute__((noinline)) Nearest wave_full_scan(const int *__restric
 // entry ties it and no bucket holds more than 8 entries.  `skip` = the killed
 // slot; slot `moved` is taken at (mx,my,mz) instead of its stored site.
 __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf, int lane, double x, double y,
-                                                    double z, int skip, int moved, double mx, double my, double mz) {
+                                                    double z, int skip, int moved, double mx, double my, double mz,
+                                                    double mzeta) {
     const CellGrid &G = d.grid;
     const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
               bk = grid_axis(z, G.z0, G.iz, G.gz);
@@ -443,23 +446,28 @@ __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf,
     const bool inb = lane < 54 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
     const int b = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
     const int cnt = d.bucket_count[b];
-    BucketEntry e[4];
+    CellEntry e[4];
+    int sl[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) e[u] = d.buckets[b * kBucketCap + grp * 4 + u];
+    for (int u = 0; u < 4; ++u) {
+        e[u] = d.buckets[b * kBucketCap + grp * 4 + u];
+        sl[u] = d.bslot[b * kBucketCap + grp * 4 + u];
+    }
     // every cell outside the 3x3x3 block is at least sqrt(lb) away: computed while the loads fly
     const double lb = grid_block_lb(G, x, y, z, 1);
-    double bd = kSentinel;
+    double bd = kSentinel, bz = 0.0;
     int bs = -1;
     bool tie = false;
     const bool overfull = inb && cnt > 8;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const bool ok = inb && grp * 4 + u < cnt && e[u].slot != skip && e[u].slot != moved;
+        const bool ok = inb && grp * 4 + u < cnt && sl[u] != skip && sl[u] != moved;
         const double dd = dist2(e[u].x, e[u].y, e[u].z, x, y, z);
         if (ok) {
             if (dd < bd) {
                 bd = dd;
-                bs = e[u].slot;
+                bs = sl[u];
+                bz = e[u].zeta;
                 tie = false;
             } else if (dd == bd && dd < kSentinel) {
                 tie = true;
@@ -471,12 +479,12 @@ __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf,
         if (dd < bd) {
             bd = dd;
             bs = moved;
+            bz = mzeta;
             tie = false;
         } else if (dd == bd && dd < kSentinel) {
             tie = true;
         }
     }
-    const double bz = d.czeta[bs >= 0 ? bs : 0];  // issued now, used after the reduction
     const unsigned long long key = (unsigned long long)__double_as_longlong(bd);
     const unsigned long long kmin = wave_min_u64(key);
     const unsigned long long who = __ballot(key == kmin);
@@ -496,8 +504,8 @@ __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf,
 // Nearest live cell for one query, one wave: grid first, full scan if unproven.
 __device__ __forceinline__ Nearest wave_nearest(const DevChain &d, const Views &v, Shared &sh, int lane, double x,
                                                 double y, double z, int skip, int moved, double mx, double my,
-                                                double mz) {
-    Nearest r = wave_grid_search(d, sh.grid_ovf != 0, lane, x, y, z, skip, moved, mx, my, mz);
+                                                double mz, double mzeta) {
+    Nearest r = wave_grid_search(d, sh.grid_ovf != 0, lane, x, y, z, skip, moved, mx, my, mz, mzeta);
     if (!r.proven) {
         if (lane == 0) atomicAdd(&sh.grid_fallbacks32, 1);
         r = wave_full_scan(d.rank, v.ord, d.cx, d.cy, d.cz, d.czeta, d.cap, sh.nslots, lane, x, y, z, skip, moved,
@@ -513,14 +521,18 @@ __device__ void grid_prefetch(const DevChain &d, Shared &sh, int lane, int actio
                               double oz, double nx, double ny, double nz) {
     const bool rm = action == tdchain::kDeath || action == tdchain::kMove;
     const bool ins = action == tdchain::kBirth || action == tdchain::kMove;
+    const bool upd = action == tdchain::kChange;  // the entry's value, in place
     int bo = 0, co = 0, pos = -1, bn = 0, cn = 0;
-    if (rm) {
+    if (rm || upd) {
         bo = grid_bucket(d.grid, ox, oy, oz);
         co = d.bucket_count[bo];
-        const int s = lane < kBucketCap ? d.buckets[bo * kBucketCap + lane].slot : -1;
+        const int s = lane < kBucketCap ? d.bslot[bo * kBucketCap + lane] : -1;
         const unsigned long long m = __ballot(lane < co && s == slot);
         pos = m ? __builtin_ctzll(m) : -1;
-        if (lane == 0 && co > 0) sh.gp_last = d.buckets[bo * kBucketCap + co - 1];
+        if (rm && lane == 0 && co > 0) {
+            sh.gp_last = d.buckets[bo * kBucketCap + co - 1];
+            sh.gp_last_slot = d.bslot[bo * kBucketCap + co - 1];
+        }
     }
     if (ins) {
         bn = grid_bucket(d.grid, nx, ny, nz);
@@ -547,15 +559,26 @@ __device__ void grid_apply(const DevChain &d, Shared &sh) {
             sh.grid_ovf = 1;
         } else {
             d.buckets[b * kBucketCap + pos] = sh.gp_last;
+            d.bslot[b * kBucketCap + pos] = sh.gp_last_slot;
             d.bucket_count[b] = co - 1;
             co -= 1;
+        }
+    }
+    if (op & 4) {  // a change: the entry's value
+        const int pos = sh.gp_pos;
+        if (pos < 0) {
+            *d.grid_overflow = 1;
+            sh.grid_ovf = 1;
+        } else {
+            d.buckets[sh.gp_bo * kBucketCap + pos].zeta = sh.g_nzeta;
         }
     }
     if (op & 2) {  // insert at the new site
         const int b = sh.gp_bn;
         const int cnt = ((op & 1) && b == sh.gp_bo) ? co : sh.gp_cn;  // a move inside one bucket
         if (cnt < kBucketCap) {
-            d.buckets[b * kBucketCap + cnt] = BucketEntry{sh.g_nx, sh.g_ny, sh.g_nz, sh.g_slot, 0};
+            d.buckets[b * kBucketCap + cnt] = CellEntry{sh.g_nx, sh.g_ny, sh.g_nz, sh.g_nzeta};
+            d.bslot[b * kBucketCap + cnt] = sh.g_slot;
             d.bucket_count[b] = cnt + 1;
         } else {
             *d.grid_overflow = 1;
@@ -666,7 +689,8 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
                 if (has_edit && e.action != tdchain::kBirth) slot_k = v.ord[e.index];
                 if (has_edit && e.action == tdchain::kDeath) skip = slot_k;  // the reduced model (:132-135)
                 if (has_edit && e.action == tdchain::kMove) moved = slot_k;  // the cell at its new site
-                const Nearest r = wave_nearest(d, v, sh, lane, x, y, z, skip, moved, e.x, e.y, e.z);
+                const Nearest r = wave_nearest(d, v, sh, lane, x, y, z, skip, moved, e.x, e.y, e.z,
+                                               moved >= 0 ? d.czeta[moved] : 0.0);
                 double val = r.z;
                 if (has_edit && e.action == tdchain::kChange && r.s == slot_k) val = e.zeta;
                 if (has_edit && e.action == tdchain::kBirth) {  // the appended cell wins only strictly (last position)
@@ -1410,7 +1434,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             if (query && wv == kWv - 1) {  // TD_inversion_function.jl:81 (birth), :146 (death)
                 const bool birth = action == tdchain::kBirth;
                 const Nearest r = wave_nearest(d, v, sh, lane, birth ? p.x : kx, birth ? p.y : ky, birth ? p.z : kz,
-                                               birth ? -1 : slot_k, -1, 0.0, 0.0, 0.0);
+                                               birth ? -1 : slot_k, -1, 0.0, 0.0, 0.0, 0.0);
                 if (lane == 0) sh.q_zeta = r.z;
             }
             __syncthreads();  // tile list complete, query answered
@@ -1565,11 +1589,11 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                 const int cnt = d.bucket_count[bucket];
                                 const int base = cnt > 0 ? atomicAdd(&sh.ob_ncand, cnt) : 0;
                                 for (int e = 0; e < cnt && base + e < kBatchCand; ++e) {
-                                    const BucketEntry &be = d.buckets[bucket * kBucketCap + e];
+                                    const CellEntry &be = d.buckets[bucket * kBucketCap + e];
                                     ex[base + e] = be.x;
                                     ey[base + e] = be.y;
                                     ez[base + e] = be.z;
-                                    es[base + e] = be.slot;
+                                    es[base + e] = d.bslot[bucket * kBucketCap + e];
                                 }
                             }
                             __syncthreads();
@@ -1662,7 +1686,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         qz = d.pz[q];
                         ray = d.pt_ray[q];
                     }
-                    const Nearest r = wave_nearest(d, v, sh, lane, qx, qy, qz, skip_s, moved_s, pp.x, pp.y, pp.z);
+                    const Nearest r =
+                        wave_nearest(d, v, sh, lane, qx, qy, qz, skip_s, moved_s, pp.x, pp.y, pp.z, zeta_killed);
                     if (lane == 0) mark(d, v, sh, q, ray, r.s, r.d, r.z);
                 }
                 if (nlist > 0) __syncthreads();
@@ -1852,7 +1877,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 if (prof_on) sh.prof[67] += clock64() - tF;  // diagnostic: decision taken
                 if (acc || (mb && sh.step_cur.decision == kDecideLater)) {
                     sh.g_op = action == tdchain::kBirth ? 2 : action == tdchain::kDeath ? 1
-                              : action == tdchain::kMove ? 3 : 0;
+                              : action == tdchain::kMove ? 3 : 4;
                     sh.g_slot = action == tdchain::kBirth ? new_slot : slot_k;
                     sh.g_ox = kx;
                     sh.g_oy = ky;
@@ -1860,6 +1885,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     sh.g_nx = pp.x;
                     sh.g_ny = pp.y;
                     sh.g_nz = pp.z;
+                    sh.g_nzeta = pp.zeta;
                     if (acc) atomicAdd((unsigned long long *)&sh.accepted[action], 1ull);
                 }
                 if (prof_on && bdec == 1) atomicAdd((unsigned long long *)&sh.prof[14], 1ull);  // rejected on bounds
@@ -1872,7 +1898,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             } else if (wv == kWv - 1 || (kWv >= 6 && wv == kWv - 2)) {
                 // wave kWv - 1: the grid data an accepted update will need; wave kWv - 2 (with 8 waves;
                 // with 4 the last wave after its prefetch): accounting and the model-size factors
-                if (wv == kWv - 1 && action != tdchain::kChange)
+                if (wv == kWv - 1)
                     grid_prefetch(d, sh, lane, action, action == tdchain::kBirth ? new_slot : slot_k, kx, ky,
                                   kz, pp.x, pp.y, pp.z);
                 if (wv == (kWv >= 6 ? kWv - 2 : kWv - 1)) {
@@ -2279,7 +2305,7 @@ __global__ __launch_bounds__(64) void k_chain_query(const DevChain *__restrict__
     if (has_edit && e.action != tdchain::kBirth) slot_k = d.order[e.index];
     if (has_edit && e.action == tdchain::kDeath) skip = slot_k;  // the reduced model (:132-135)
     if (has_edit && e.action == tdchain::kMove) moved = slot_k;  // the cell at its new site
-    Nearest r = wave_nearest(d, v, sh, lane, x, y, z, skip, moved, e.x, e.y, e.z);
+    Nearest r = wave_nearest(d, v, sh, lane, x, y, z, skip, moved, e.x, e.y, e.z, moved >= 0 ? d.czeta[moved] : 0.0);
     double val = r.z;
     if (has_edit && e.action == tdchain::kChange && r.s == slot_k) val = e.zeta;
     if (has_edit && e.action == tdchain::kBirth) {  // the appended cell: last position, wins only strictly
