@@ -64,7 +64,10 @@ def main():
                       "epilogue cycles per launch": round(tot[77] / max(tot[78], 1), 1),
                       "launches": int(tot[78] / C), "by_action": by_action,
                       # free per-action slots (16 + 10 a + 9): sub-stamps of a diagnostic build, else 0
-                      "sub_slots": {k: round(tot[k] / n, 1) for k in (11, 15, 75, 25, 35, 45, 55)}}, indent=1))
+                      "sub_slots": {k: round(tot[k] / n, 1) for k in (11, 15, 75, 25, 35, 45, 55)},
+                      # per proposal: rejected on bounds, chi^2 tail terms, exact decisions, F cycles to the
+                      # scan / the decision, hit tiles, points seen, changed points, changed rays
+                      "diag": {k: round(tot[k] / n, 4) for k in (14, 64, 65, 66, 67, 68, 69, 70, 71)}}, indent=1))
 
 
 if __name__ == "__main__":
