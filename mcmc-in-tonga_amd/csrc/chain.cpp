@@ -609,13 +609,20 @@ volatile long long *vol(long long *p) { return p; }
 std::atomic<int> g_post_delay_ms{0};
 constexpr int kExitedEarly = -1;  // server_post: the kernel returned before answering
 
+// Publish the command written into the mailbox: its check, then seq (the kernel reads them all
+// in one poll and takes the command only when the check matches)
+void post_seq(Mailbox *m, long long sq) {
+    m->check = mailbox_check(m, sq);
+    std::atomic_thread_fence(std::memory_order_release);
+    *vol(&m->seq) = sq;
+}
+
 int server_stop(td_chain *ch) {
     if (!ch || !ch->srv_running) return TD_OK;
     Mailbox *m = ch->mb_host;
     if (!*vol(&m->exited)) {
         m->type = kCmdQuit;
-        std::atomic_thread_fence(std::memory_order_release);
-        *vol(&m->seq) = m->seq + 1;
+        post_seq(m, m->seq + 1);
     }
     hipError_t e = hipStreamSynchronize(ch->srv_stream);  // the kernel returns (QUIT, or its idle watchdog)
     ch->srv_running = false;
@@ -658,8 +665,7 @@ int server_start(td_chain *ch) {
 int server_post(td_chain *ch) {
     Mailbox *m = ch->mb_host;
     const long long sq = m->seq + 1;
-    std::atomic_thread_fence(std::memory_order_release);
-    *vol(&m->seq) = sq;
+    post_seq(m, sq);
     const auto t0 = std::chrono::steady_clock::now();
     for (long long spin = 0;; ++spin) {
         if (*vol(&m->done) == sq) break;

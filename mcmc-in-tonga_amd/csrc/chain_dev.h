@@ -18,6 +18,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 
 #include "chain_logic.h"
@@ -145,12 +146,29 @@ struct Mailbox {
     ScriptStep step[kMaxScript];
     double q[3];
     ScriptStep qedit;
+    // mailbox_check(seq, words 1 .. check - 1): the kernel polls seq and payload in one read and takes
+    // the command only when this matches (a poll may catch the words mid-write)
+    unsigned long long check;
     // device -> host
     long long done;    // seq of the last command answered
     long long exited;  // the kernel has returned (its state is written back)
     double qval;
     long long diag[4];  // diagnostic: shader cycles and 100 MHz ticks of the last busy interval, polls
 };
+
+// The command's words (seq first, check last) and their check: each payload word mixed with its
+// position and the seq, xor-combined (the kernel: one word per lane, one DPP reduction).
+constexpr int kMailboxCheckWord = (int)(offsetof(Mailbox, check) / sizeof(long long));
+__host__ __device__ inline unsigned long long mailbox_word_mix(unsigned long long w, int i, long long seq) {
+    return tdchain::swap_mix64(w ^ ((unsigned long long)i * 0x9E3779B97F4A7C15ull) ^
+                               ((unsigned long long)seq * 0xD1B54A32D192ED03ull));
+}
+inline unsigned long long mailbox_check(const Mailbox *m, long long seq) {
+    const unsigned long long *w = reinterpret_cast<const unsigned long long *>(m);
+    unsigned long long h = 0;
+    for (int i = 1; i < kMailboxCheckWord; ++i) h ^= mailbox_word_mix(w[i], i, seq);
+    return h;
+}
 
 // Resident tempering rounds (td_rounds_*, chain.cpp): a td_chain_run_batch
 // launch that stays resident across swap rounds.  Every K proposals each

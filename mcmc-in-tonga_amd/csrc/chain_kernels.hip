@@ -663,22 +663,36 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
         mb_store(&mb->diag[0], clock64() - sh.srv_busy_c);
         mb_store(&mb->diag[1], t0 - sh.srv_busy_w);
     }
+    static_assert(kMailboxCheckWord == kWords - 1, "the check is the command's last word");
     long long polls = 0;
     while (true) {
-        const long long sq = mb_load(&mb->seq);
+        // every poll reads the whole command, one word per lane (as cheap as seq alone: one round
+        // trip); a new seq is taken only with a matching check -- the poll may have caught the
+        // host between its words (then the next poll reads them again)
+        // (no system-scope acquire: the command is read through system-scope atomics, and one
+        // would invalidate this XCD's L2, the chain's working set, at every call)
+        const long long w = lane < kWords ? mb_load(reinterpret_cast<const long long *>(mb) + lane) : 0;
+        const long long sq = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(w >> 32), 0) << 32) |
+                                         (unsigned)__builtin_amdgcn_readlane((int)w, 0));
         ++polls;
-        if (sq != seen) {
+        bool fresh = sq != seen;
+        if (fresh) {  // (a torn read: not yet -- the next poll reads the words again)
+            const unsigned long long h =
+                wave_xor_u64(lane >= 1 && lane < kWords - 1 ? mailbox_word_mix((unsigned long long)w, lane, sq) : 0ull);
+            const unsigned long long chk =
+                ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(w >> 32), kWords - 1) << 32) |
+                (unsigned)__builtin_amdgcn_readlane((int)w, kWords - 1);
+            fresh = h == chk;
+        }
+        if (fresh) {
             seen = sq;
             if (lane == 0) {
                 sh.srv_busy_c = clock64();
                 sh.srv_busy_w = (long long)wall_clock64();
                 mb_store(&mb->diag[2], polls);
             }
-            // (no system-scope acquire: the command is read through system-scope atomics, and one
-            // would invalidate this XCD's L2, the chain's working set, at every call)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            // the whole command in one round trip: one mailbox word per lane, into LDS
-            if (lane < kWords) sh.mbox[lane] = mb_load(reinterpret_cast<const long long *>(mb) + lane);
+            if (lane < kWords) sh.mbox[lane] = w;
             wave_sync_lds();
             const Mailbox &c = *reinterpret_cast<const Mailbox *>(sh.mbox);
             if (c.type == kCmdQuery) {

@@ -64,6 +64,18 @@ __device__ __forceinline__ unsigned long long row_max_u64(unsigned long long v) 
     v = umax64(v, dpp_u64<0x118, 0xf>(v, 0ull));
     return v;
 }
+// xor over the 64 lanes, to every lane
+__device__ __forceinline__ unsigned long long wave_xor_u64(unsigned long long v) {
+    v ^= dpp_u64<0x111, 0xf>(v, 0ull);
+    v ^= dpp_u64<0x112, 0xf>(v, 0ull);
+    v ^= dpp_u64<0x114, 0xf>(v, 0ull);
+    v ^= dpp_u64<0x118, 0xf>(v, 0ull);
+    v ^= dpp_u64<0x142, 0xa>(v, 0ull);  // row_bcast:15
+    v ^= dpp_u64<0x143, 0xc>(v, 0ull);  // row_bcast:31 -> lane 63: the whole wave
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);

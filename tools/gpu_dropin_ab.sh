@@ -1,0 +1,12 @@
+set -o pipefail
+out=gpurun_out/dab; mkdir -p $out
+for k in 1 2; do
+  for v in base head; do
+    if [ $v = base ]; then export TD_LIB_PATH=$PWD/ab/libtdstar_base.so; else unset TD_LIB_PATH; fi
+    timeout -k 10 120 python tools/dropin_only.py > $out/$v$k.json 2>&1 || { echo "$v failed"; tail $out/$v$k.json; exit 1; }
+    python -c "import json; d=json.loads(open('$out/$v$k.json').read().strip().splitlines()[-1]); i=d['incremental']; print('$v', i['us_per_proposal'], {k: v for k, v in i['breakdown_us_per_proposal'].items() if 'round_trip' in k or 'busy' in k})"
+  done
+done
+unset TD_LIB_PATH
+timeout -k 10 600 python -u -m pytest tests/test_gpu_incremental.py tests/test_gpu_chain.py -x -q --timeout 300 --timeout-method thread > $out/tests.log 2>&1 || { echo tests failed; tail -30 $out/tests.log; exit 1; }
+tail -2 $out/tests.log

@@ -24,7 +24,43 @@
 __device__ long long ld_sys(const long long *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 __device__ void st_sys(long long *p, long long v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 
-// echo: wait for cmd[0] != last, write done = cmd[0]; quit on a negative seq or 2 s of silence
+// echo: wait for cmd[0] != last, write done = cmd[0]; quit on a negative seq or 2 s of silence.
+// mode bit 0: s_sleep between polls; bit 1: after seeing the seq, read a 24-word payload in a
+// second round trip (the chain server's command read); bit 2: write a result word and wait for
+// its acknowledgment before done (the server's answer); bit 3: every poll reads the 24 words
+__global__ void k_echo_full(const long long *cmd, long long *done, int mode) {
+    const int lane = threadIdx.x;
+    long long last = 0;
+    long long t0 = (long long)wall_clock64();
+    long long sink = 0;
+    while (true) {
+        long long w = 0;
+        if (mode & 8) w = lane < 24 ? ld_sys(cmd + lane) : 0;
+        else w = ld_sys(cmd);
+        const long long s = __shfl(w, 0);
+        if (s != last) {
+            if (s < 0) break;
+            last = s;
+            if (mode & 2) {
+                const long long p = lane < 24 ? ld_sys(cmd + lane) : 0;
+                sink += p;
+            }
+            if (lane == 0) {
+                if (mode & 4) {
+                    st_sys(done + 2, s + sink);
+                    __builtin_amdgcn_s_waitcnt(0);
+                }
+                st_sys(done, s);
+            }
+            t0 = (long long)wall_clock64();
+            continue;
+        }
+        if ((long long)wall_clock64() - t0 > 200000000ll) break;
+        if (mode & 1) __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0 && sink == 42) st_sys(done + 3, sink);
+}
+
 __global__ void k_echo(const long long *cmd, long long *done, int sleep_mode) {
     if (threadIdx.x != 0) return;
     long long last = 0;
@@ -48,7 +84,8 @@ double run(long long *cmd_host_view, const long long *cmd_dev, long long *done_h
     *(volatile long long *)cmd_host_view = 0;
     *(volatile long long *)done_host = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    hipLaunchKernelGGL(k_echo, dim3(1), dim3(64), 0, 0, cmd_dev, done_dev, sleep_mode);
+    if (sleep_mode >= 16) hipLaunchKernelGGL(k_echo_full, dim3(1), dim3(64), 0, 0, cmd_dev, done_dev, sleep_mode - 16);
+    else hipLaunchKernelGGL(k_echo, dim3(1), dim3(64), 0, 0, cmd_dev, done_dev, sleep_mode);
     // warm
     for (int i = 1; i <= 100; ++i) {
         *(volatile long long *)cmd_host_view = i;
@@ -84,6 +121,9 @@ int main() {
     for (int sm = 0; sm < 2; ++sm)
         std::printf("A pinned host command, sleep %d: %.3f us per round trip\n", sm,
                     run(cmdA, cmdA_dev, done_host, done_dev, 2000, sm));
+    for (int mode : {16, 16 + 2, 16 + 4, 16 + 6, 16 + 8, 16 + 12})
+        std::printf("A pinned host command, server-like mode %d (2: payload read, 4: acked result, 8: wide poll): %.3f us\n",
+                    mode - 16, run(cmdA, cmdA_dev, done_host, done_dev, 2000, mode));
     // B: command in fine-grained device memory, written by the host
     long long *cmdB = nullptr;
     hipError_t e = hipExtMallocWithFlags((void **)&cmdB, 4096, hipDeviceMallocFinegrained);
