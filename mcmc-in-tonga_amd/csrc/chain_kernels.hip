@@ -280,7 +280,7 @@ __host__ __device__ inline LdsPlan lds_plan(int ntiles, int n, int cap, bool sma
                                             bool rays_lds = true) {
     LdsPlan L{};
     size_t o = align16(sizeof(Shared));
-    L.scratch = o; o += align16(sizeof(double) * waves * 96);
+    L.scratch = o; o += align16(sizeof(double) * waves * (small ? 96 : 192));  // (HBM layout: two rays a wave)
     L.draws = o; o += align16(sizeof(tdchain::Draws) * 64);                     // 64 iterations ahead
     if (!small || kSmallWalk) {  // the chi^2 walk's event words (exact_sum.h): static ones, kept; changed rays
         L.smask = o; o += align16(sizeof(unsigned long long) * delta_words(n));
@@ -1709,51 +1709,97 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 // ================= phase E: t* of the rays that changed =================
                 const int nr = sh.n_rays;
                 const OverlayZeta oz{d.cand_flag, d.cand_z, d.zeta0};
-                // rays in HBM: a wave's rays' offsets, tS, sigma and old terms, one per lane,
-                // in one round of loads before its first sum (the 64 first; more: per ray)
-                int ra = 0, s0a = 0, e0a = 0;
-                double tsa = 0.0, sga = 0.0, ota = 0.0;
-                if (!RLDS && wv + kWv * lane < nr && lane < 64) {
-                    ra = v.ray_at(wv + kWv * lane);
-                    s0a = v.ray_off[ra];
-                    e0a = v.ray_off[ra + 1];
-                    tsa = v.tS[ra];
-                    sga = v.sig[ra];
-                    ota = v.term[ra];
-                }
-                for (int rr = wv, j = 0; rr < nr; rr += kWv, ++j) {
-                    int r, s0, npr;
-                    double tsr, sgr, old_term;
-                    if (!RLDS && j < 64) {
-                        r = __builtin_amdgcn_readlane(ra, j);
-                        s0 = __builtin_amdgcn_readlane(s0a, j);
-                        npr = __builtin_amdgcn_readlane(e0a, j) - s0;
-                        tsr = readlane_f64(tsa, j);
-                        sgr = readlane_f64(sga, j);
-                        old_term = readlane_f64(ota, j);
-                    } else {
-                        r = v.ray_at(rr);
-                        s0 = v.ray_off[r];
-                        npr = v.ray_off[r + 1] - s0;
-                        tsr = v.tS[r];  // with the offsets
-                        sgr = v.sig[r];
-                        old_term = v.term[r];
+                // the t* of a changed ray and its chi^2 term (MCsub.jl:147-171), kept beside the old
+                auto ray_done = [&](int r, double val, double tsr, double sgr, double old_term, int npr) {
+                    v.cptS[r] = val;
+                    const double df = val - tsr;
+                    const double sg = sgr;
+                    v.cterm[r] = old_term;                       // kept to undo a rejection
+                    const double nterm = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
+                    v.term[r] = nterm;
+                    if constexpr (!RLDS) {  // (the running total: any order; rays in LDS re-add them all)
+                        atomicAdd(&sh.dsum, nterm - old_term);
+                        atomicAdd(&sh.dabs, fabs(nterm) + fabs(old_term));
                     }
-                    const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
-                    if (lane == 0) {
-                        v.cptS[r] = val;
-                        const double df = val - tsr;
-                        const double sg = sgr;
-                        v.cterm[r] = old_term;                       // kept to undo a rejection
-                        const double nterm = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
-                        v.term[r] = nterm;
-                        if constexpr (!RLDS) {  // (the running total: any order; rays in LDS re-add them all)
-                            atomicAdd(&sh.dsum, nterm - old_term);
-                            atomicAdd(&sh.dabs, fabs(nterm) + fabs(old_term));
+                    atomicAdd(&sh.ray_pts, npr);
+                    if constexpr (WALK)  // an event of the walk (scripted steps: the decisions on bounds need none)
+                        if (nscript) atomicOr(&cmask[r >> 6], 1ull << (r & 63));
+                };
+                if constexpr (!SMALL) {
+                    // the large geometries (~15 changed rays a proposal, every load from HBM): two rays per
+                    // wave at a time, one per half (ray_sum.h half_ray_sum), their loads in one round trip.
+                    // Lane l holds the offsets, tS, sigma and old term of the wave's ray of turn l / 2,
+                    // half l % 2 (one round of loads before the first sum; past 32 turns: per ray)
+                    const int half = lane >> 5, hl = lane & 31;
+                    const int mine = 2 * wv + (lane & 1) + 2 * kWv * (lane >> 1);
+                    int ra = 0, s0a = 0, e0a = 0;
+                    double tsa = 0.0, sga = 0.0, ota = 0.0;
+                    if (mine < nr) {
+                        ra = v.ray_at(mine);
+                        s0a = v.ray_off[ra];
+                        e0a = v.ray_off[ra + 1];
+                        tsa = v.tS[ra];
+                        sga = v.sig[ra];
+                        ota = v.term[ra];
+                    }
+                    double *hs = reinterpret_cast<double *>(lds + L.scratch) + wv * 192 + half * 96;
+                    for (int base = 2 * wv, j = 0; base < nr; base += 2 * kWv, ++j) {
+                        const int rr = base + half;
+                        const bool have = rr < nr;
+                        int r = 0, s0 = 0, npr = 0;
+                        double tsr = 0.0, sgr = 0.0, old_term = 0.0;
+                        if (j < 32) {  // (wave-uniform)
+                            const int src = 2 * j + half;
+                            r = __shfl(ra, src);
+                            s0 = __shfl(s0a, src);
+                            npr = __shfl(e0a, src) - s0;
+                            tsr = __shfl(tsa, src);
+                            sgr = __shfl(sga, src);
+                            old_term = __shfl(ota, src);
+                        } else if (have) {
+                            r = v.ray_at(rr);
+                            s0 = v.ray_off[r];
+                            npr = v.ray_off[r + 1] - s0;
+                            tsr = v.tS[r];
+                            sgr = v.sig[r];
+                            old_term = v.term[r];
                         }
-                        atomicAdd(&sh.ray_pts, npr);
-                        if constexpr (WALK)  // an event of the walk (scripted steps: the decisions on bounds need none)
-                            if (nscript) atomicOr(&cmask[r >> 6], 1ull << (r & 63));
+                        const double val = half_ray_sum(hl, d.w, oz, s0, have ? npr : 0, hs);
+                        if (have && hl == 0) ray_done(r, val, tsr, sgr, old_term, npr);
+                    }
+                } else {
+                    // rays in HBM: a wave's rays' offsets, tS, sigma and old terms, one per lane,
+                    // in one round of loads before its first sum (the 64 first; more: per ray)
+                    int ra = 0, s0a = 0, e0a = 0;
+                    double tsa = 0.0, sga = 0.0, ota = 0.0;
+                    if (!RLDS && wv + kWv * lane < nr && lane < 64) {
+                        ra = v.ray_at(wv + kWv * lane);
+                        s0a = v.ray_off[ra];
+                        e0a = v.ray_off[ra + 1];
+                        tsa = v.tS[ra];
+                        sga = v.sig[ra];
+                        ota = v.term[ra];
+                    }
+                    for (int rr = wv, j = 0; rr < nr; rr += kWv, ++j) {
+                        int r, s0, npr;
+                        double tsr, sgr, old_term;
+                        if (!RLDS && j < 64) {
+                            r = __builtin_amdgcn_readlane(ra, j);
+                            s0 = __builtin_amdgcn_readlane(s0a, j);
+                            npr = __builtin_amdgcn_readlane(e0a, j) - s0;
+                            tsr = readlane_f64(tsa, j);
+                            sgr = readlane_f64(sga, j);
+                            old_term = readlane_f64(ota, j);
+                        } else {
+                            r = v.ray_at(rr);
+                            s0 = v.ray_off[r];
+                            npr = v.ray_off[r + 1] - s0;
+                            tsr = v.tS[r];  // with the offsets
+                            sgr = v.sig[r];
+                            old_term = v.term[r];
+                        }
+                        const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
+                        if (lane == 0) ray_done(r, val, tsr, sgr, old_term, npr);
                     }
                 }
                 __syncthreads();

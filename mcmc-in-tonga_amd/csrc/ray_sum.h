@@ -152,6 +152,78 @@ __device__ double wave_ray_sum(int lane, const double *__restrict__ w, const Z &
     return res;
 }
 
+// wave_ray_sum on HALF a wave: lanes 0..31 sum one ray and lanes 32..63 another, in the same
+// instructions -- two rays' loads in one round trip (the rays in HBM, where a ray's loads are
+// the phase's latency).  hl = lane % 32; the half's result on its lane hl == 0.  The same terms
+// in the same association as wave_ray_sum (a 32-lane accumulator step is what it uses too).
+// scratch: 96 doubles per half.  np = 0: nothing (the half has no ray).
+template <class Z>
+__device__ double half_ray_sum(int hl, const double *__restrict__ w, const Z &zeta, int s0, int np, double *scratch) {
+    double *acc_sh = scratch;       // 32
+    double *seq_sh = scratch + 32;  // 64
+    const int L = np > 0 ? np - 1 : 0;
+    double res = 0.0;  // sum over an empty array
+    if (L == 1) {
+        res = seg_term_z(w, zeta, s0);
+    } else if (L >= 2 && L < 16) {
+        if (hl < L) seq_sh[hl] = seg_term_z(w, zeta, s0 + hl);
+        wave_sync_lds();
+        if (hl == 0) {
+            double s = seq_sh[0] + seq_sh[1];
+            for (int a = 2; a < L; ++a) s = s + seq_sh[a];
+            res = s;
+        }
+    } else if (L >= 16 && L <= 1024) {
+        const int T = L - 2;
+        const int Q = T >= 32 ? T / 32 : 0;
+        const int tail0 = 2 + 32 * Q;
+        const int ntail = L - tail0;  // <= 31
+        if (Q > 0) {
+            double acc = 0.0;
+            if (hl == 0) acc = seg_term_z(w, zeta, s0) + seg_term_z(w, zeta, s0 + 1);
+            for (int q0 = 0; q0 < Q; q0 += 4) {
+                double t[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    t[u] = q0 + u < Q ? seg_term_z(w, zeta, s0 + 2 + 32 * (q0 + u) + hl) : 0.0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (q0 + u < Q) acc = acc + t[u];
+            }
+            acc_sh[hl] = acc;
+        }
+        if (hl < ntail) seq_sh[hl] = seg_term_z(w, zeta, s0 + tail0 + hl);
+        wave_sync_lds();
+        if (hl == 0) {
+            double v;
+            if (Q > 0) {
+                double r[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) r[j] = acc_sh[j];
+#pragma unroll
+                for (int k = 1; k < 4; ++k)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) r[j] = acc_sh[k * 8 + j] + r[j];
+                r[0] = r[0] + r[4];
+                r[1] = r[1] + r[5];
+                r[2] = r[2] + r[6];
+                r[3] = r[3] + r[7];
+                r[0] = r[0] + r[2];
+                r[1] = r[1] + r[3];
+                v = r[0] + r[1];
+            } else {
+                v = seg_term_z(w, zeta, s0) + seg_term_z(w, zeta, s0 + 1);
+            }
+            for (int a = 0; a < ntail; ++a) v = v + seq_sh[a];
+            res = v;
+        }
+    } else if (L > 1024) {
+        if (hl == 0) res = julia_pairwise_lane(w, zeta, s0, L);
+    }
+    wave_sync_lds();  // scratch may be reused by this wave right after
+    return res;
+}
+
 struct PlainZeta {
     const double *z;
     __device__ __forceinline__ double operator()(int k) const { return z[k]; }
