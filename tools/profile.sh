@@ -18,6 +18,10 @@ trace_only() {  # name, bench args...: kernel trace only (PMC passes serialize t
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name/trace -o run -- python3 bench.py "$@" > $OUT/$name/trace.log 2>&1 || return 1
 }
 mkdir -p $OUT/single $OUT/many $OUT/packed $OUT/stress $OUT/config4
+if [ -n "$2" ]; then  # one pass only: tools/profile.sh TAG stress
+    [ "$2" = stress ] && { run stress --steps 1 --warmup 0 --iters-per-step 10 --no-cpu-baseline --no-full-evaluate --no-dropin --no-config4 --batch-chains 0 || exit 1; }
+    exit 0
+fi
 run single --steps 3 --warmup 1 --no-cpu-baseline --batch-chains 0 --no-stress --no-dropin --no-config4 && \
 run many --steps 2 --warmup 1 --no-cpu-baseline --no-full-evaluate --no-dropin --no-config4 --no-stress --batch-chains 0 --chains-per-gpu 256 --iters-per-step 5000 && \
 run packed --steps 1 --warmup 0 --iters-per-step 10 --no-cpu-baseline --no-full-evaluate --no-dropin --no-config4 --no-stress --batch-chains 256 --batch-iters 5000 && \
