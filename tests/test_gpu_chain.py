@@ -540,3 +540,45 @@ def test_two_chains_per_cu_variant_follows_host(tt, ds, ctx, mode):
         ref.close()
     for c in host + eight + four + many + [solo]:
         c.close()
+
+
+def test_hbm_layout_edge_rays_follow_host_engine(tt):
+    """Rays of 1, 2, 3, 16, 17, 18, 34, 35, 140 and 2100 points (every branch of
+    the two-rays-per-wave sum, ray_sum.h half_ray_sum, down to Julia's pairwise
+    split above 1024 terms), several crossing one region so that proposals
+    change many rays at once, in the HBM layout (k_chain_run<false>) against
+    the host engine, bit for bit."""
+    rng = np.random.default_rng(11)
+    lens = [1, 2, 3, 16, 17, 18, 34, 35, 140, 2100, 17, 35, 140, 3, 34, 18, 2]
+    m = max(lens)
+    rays = []
+    for k, n in enumerate(lens):
+        a = rng.uniform([-50.0, -50.0, 100.0], [750.0, 350.0, 600.0])
+        b = np.array([350.0, 150.0, 300.0]) + rng.normal(0.0, 40.0, 3)  # through one region
+        t = np.linspace(0.0, 1.0, n)[:, None]
+        rays.append(a + t * (b - a) * (2.0 if k % 2 else 1.0))
+    nr = len(rays)
+    X, Y, Z = (np.full((m, nr), np.nan) for _ in range(3))
+    for i, r in enumerate(rays):
+        X[:len(r), i], Y[:len(r), i], Z[:len(r), i] = r[:, 0], r[:, 1], r[:, 2]
+    U = np.where(np.isnan(X), np.nan, 0.1 + 0.001 * np.nan_to_num(Z))
+    L, Uu = tt.segments(X, Y, Z, U)
+    tS = np.linspace(0.1, 0.5, nr)
+    sig = np.linspace(0.05, 0.3, nr)
+    ds2 = tt.DataStruct(tS, tS, tS, tS, sig, tS, tS, tS, tS, tS, tS, tS, tS, tS, tS, tS, tS, X, Y, Z, L, Uu, U)
+    c2 = tt.TdContext.from_datastruct(ds2)
+    prm = tt.define_TDstructrure().replace(max_cells=400)
+    model = tt.random_model(250, 9)
+    dev = make(tt, c2, prm, model, 9, tt.TD_ENGINE_DEVICE)
+    assert tt.lib().tdt_chain_set_lds_mode(dev.h, 1) == 0
+    host = make(tt, c2, prm, model, 9, tt.TD_ENGINE_HOST)
+    for _ in range(3):
+        dev.run(150)
+        host.run(150)
+        assert dev.stats()["phi"] == host.stats()["phi"]
+        assert dev.stats()["accepted"] == host.stats()["accepted"]
+    assert sum(dev.stats()["accepted"]) > 20  # (the models really moved)
+    assert same_models(dev.model(), host.model())
+    dev.close()
+    host.close()
+    c2.close()
