@@ -68,6 +68,9 @@ struct ScriptStep {
     int index;       // Julia position (0-based) of the killed / changed / moved cell
     double x, y, z;  // birth site / move target
     double zeta;     // birth / change value
+    // death / change / move: the cell at `index` before the step, (x, y, z, zeta) -- from the
+    // host's copy of the model, bit-equal to the chain's: the proposal reads no cell array
+    double old[4];
     int decision;
     int pad;
 };

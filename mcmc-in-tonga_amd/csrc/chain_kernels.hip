@@ -162,8 +162,7 @@ __device__ __forceinline__ void make_proposal(PState &o, const tdchain::Params &
 // active and valid, no draws; birth's zeta is given (birth_zeta is not called).
 template <class SlotAt>
 __device__ __forceinline__ void script_proposal(PState &o, const ScriptStep &st, int nfree, int nslots,
-                                               const int *free_slots, const double *cx, const double *cy,
-                                               const double *cz, const double *czeta, SlotAt slot_at) {
+                                               const int *free_slots, SlotAt slot_at) {
     Proposal q{};
     q.action = st.action;
     q.active = 1;
@@ -178,10 +177,10 @@ __device__ __forceinline__ void script_proposal(PState &o, const ScriptStep &st,
     if (q.action != tdchain::kBirth) {
         const int s = slot_at(st.index);
         o.slot_k = s;
-        o.kx = cx[s];
-        o.ky = cy[s];
-        o.kz = cz[s];
-        o.zeta_killed = czeta[s];
+        o.kx = st.old[0];  // the cell's values came with the step (a round trip to the cell arrays saved)
+        o.ky = st.old[1];
+        o.kz = st.old[2];
+        o.zeta_killed = st.old[3];
         if (q.action == tdchain::kChange) {  // the site stays; only zeta is new
             q.x = o.kx;
             q.y = o.ky;
@@ -237,7 +236,7 @@ struct Shared {
     long long rseq;
     int rK, rskip;
     long long srv_seq, srv_busy_c, srv_busy_w;
-    long long mbox[32];  // server mode: the last command read from the mailbox
+    long long mbox[40];  // server mode: the last command read from the mailbox
     OrphanRec orph[kOrphanLds];
     DeltaSegs dseg;  // rays in HBM: phase F's new chi^2 partial sums as segments over the old ones
     long long prof[kProfSlots], t_last, t_iter;  // diagnostic phase stamps
@@ -1188,7 +1187,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         if (lane == 0 && iters > 0 && !((mb || rbx) && sh.srv_quit)) {
             if (nscript) {
                 sh.step_cur = mb ? sh.srv_step[sh.srv_k++] : sa.step[0];
-                script_proposal(sh.ps[0], sh.step_cur, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz, d.czeta,
+                script_proposal(sh.ps[0], sh.step_cur, sh.nfree, sh.nslots, d.free_slots,
                                 [&](int pos) { return v.ord[pos]; });
             }
             else
@@ -2257,8 +2256,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         };
                         if (nscript) {
                             sh.step_cur = mb ? sh.srv_step[sh.srv_k++] : sa.step[it + 1];
-                            script_proposal(sh.ps[cur_r], sh.step_cur, sh.nfree, sh.nslots, d.free_slots, d.cx,
-                                            d.cy, d.cz, d.czeta, slot_at);
+                            script_proposal(sh.ps[cur_r], sh.step_cur, sh.nfree, sh.nslots, d.free_slots, slot_at);
                         }
                         else
                             make_proposal(sh.ps[cur_r], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots,

@@ -229,6 +229,20 @@ int classify(const double *const in[4], int64_t M, const View &base, ScriptStep 
     return -1;
 }
 
+// The step as the device takes it: with the edited cell's values before it, read from `base`
+// (the model the step applies to, the chain's model bit for bit).  The host's own copies of
+// steps (td_shadow::e) keep them zero, as classify leaves them, so they compare as edits.
+ScriptStep posted(ScriptStep e, const Cells &base) {
+    if (e.action != 1) {
+        const size_t k = (size_t)e.index;
+        e.old[0] = base.x[k];
+        e.old[1] = base.y[k];
+        e.old[2] = base.z[k];
+        e.old[3] = base.zeta[k];
+    }
+    return e;
+}
+
 bool all_sane(const double *const in[4], int64_t n) {
     for (int64_t i = 0; i < n; ++i)
         if (!sane(in[0][i]) || !sane(in[1][i]) || !sane(in[2][i]) || !std::isfinite(in[3][i])) return false;
@@ -348,7 +362,7 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
         if (s->dev_pending) {
             decision = 1;  // Julia went on from Q: the device commits its pending overlay
         } else {
-            ScriptStep c = s->e;
+            ScriptStep c = posted(s->e, s->B);
             c.decision = 1;  // re-evaluate and commit Q first
             steps[nsteps++] = c;
         }
@@ -373,7 +387,7 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
     }
     lap.stop();
     e2.decision = srv ? kDecideLater : 0;
-    steps[nsteps++] = e2;
+    steps[nsteps++] = posted(e2, s->B);
     s->ptSQ.assign((size_t)n, 0.0);
     int rc = srv ? shadow_server_eval(s->ch, decision, steps, nsteps, s->ptSB.data(), &s->phiQ, s->ptSQ.data())
                  : shadow_chain_script(s->ch, steps, nsteps, s->ptSB.data(), &s->phiQ, s->ptSQ.data());
