@@ -164,14 +164,67 @@ def parse():
     ap.add_argument("--config4-rounds", type=int, default=300, help="timed swap rounds of the config-4 blocks")
     ap.add_argument("--stress-iters", type=int, default=2000, help="timed proposals of the stress chain(s)")
     ap.add_argument("--no-phases", action="store_true", help="skip the stamped phase-cycle run")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher self-test: the ranks meet over gloo and rank 0 prints the world it saw "
+                         "(no GPU call; tests/test_bench_launch.py)")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N fresh
+    rank processes through torch.distributed.run (one per GPU, rendezvous on
+    127.0.0.1) and wait for them.  Called before anything touches the GPU
+    (this process imports neither torch nor the library), so every rank
+    initialises its own device.  Rank 0's stdout -- the JSON line -- passes
+    straight through; the exit code is torch.distributed.run's, which is
+    non-zero when any rank failed (the reference's chains are one `pmap`
+    worker each, main_inversion.jl:15)."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + argv
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(world, rank):
+    """The launcher self-test: no GPU, gloo only.  Every rank contributes one;
+    rank 0 prints the world size and the sum."""
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    t = torch.ones(1, dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": int(t.item()),
+                          "pid_parent": os.getppid()}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", 0))
     local = int(os.environ.get("LOCAL_RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != a.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks" % (a.gpus, world))
+    if a.launch_check:
+        launch_check(world, rank)
+        return
     dist = None
     if world > 1:
         import torch
@@ -867,13 +920,23 @@ def ingest_trilinear(tt):
 
 
 def host_cores():
-    """The host cores this job may use: the box exports its CPU share in
-    OMP_NUM_THREADS (16); os.cpu_count() reports the whole machine."""
+    """The host cores this job may use, read from the OS: the CPUs in this
+    process's affinity mask (os.sched_getaffinity), capped by the CPU share
+    the box exports in OMP_NUM_THREADS when that is smaller (the GPU box's
+    mask and os.cpu_count() show the whole machine, its share is 16).
+    Returns (cores used, the facts they were chosen from)."""
     try:
-        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    try:
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
     except ValueError:
-        n = 0
-    return max(1, min(n if n > 0 else 16, os.cpu_count() or 1))
+        omp = 0
+    used = min(aff, omp) if omp > 0 else aff
+    src = "OMP_NUM_THREADS (the job's CPU share)" if 0 < omp < aff else "os.sched_getaffinity(0)"
+    return max(1, used), {"sched_getaffinity": aff, "os_cpu_count": os.cpu_count(),
+                          "OMP_NUM_THREADS": omp if omp > 0 else None, "cores_from": src}
 
 
 def cpu_baseline(ds, model, seconds, tt=None):
@@ -906,7 +969,7 @@ def cpu_baseline(ds, model, seconds, tt=None):
         return sum(counts), time.perf_counter() - t0
 
     n1, el1 = leg(1, seconds * 0.5)
-    cores = host_cores()
+    cores, core_facts = host_cores()
     nc, elc = leg(cores, seconds * 0.5)
     aux = {}
     if tt is not None:  # the CPU legs of SURVEY 8f rows 2 and 4: the checker's numpy restatements, one core
@@ -924,7 +987,8 @@ def cpu_baseline(ds, model, seconds, tt=None):
         oracle_np.trilinear(xs, ys, zs, vals, px, py, pz)
         aux["ingest_trilinear"] = {"ms": round((time.perf_counter() - t0) * 1e3, 1), "cores": 1,
                                    "kind": "port (numpy)", "sample": "all %d points" % len(px)}
-    return {"value": round(nc / elc, 3), "unit": "proposals/s", "cores": cores, "kind": "port", "aux": aux,
+    return {"value": round(nc / elc, 3), "unit": "proposals/s", "cores": cores, "host": core_facts,
+            "kind": "port", "aux": aux,
             "single_core_value": round(n1 / el1, 3),
             "sample": "full evaluates (oracle/tstar_oracle.c, scalar FP64, -O2) of the same 381-ray x %d-cell "
                       "model, one chain per core: %d in %.1f s on %d cores, %d in %.1f s on 1 core; the reference "

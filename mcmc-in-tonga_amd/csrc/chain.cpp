@@ -76,7 +76,8 @@ struct td_rounds {
     std::vector<char> force_exit;  // testing (tdt_rounds_force_exit): one-shot, per chain
     // exchange rounds (td_rounds_exchange, chain_dev.h RoundX): buffers made on first use
     int x_R = 0;                  // replicas the buffers are sized for
-    double *x_in = nullptr, *x_out = nullptr, *x_temps = nullptr;  // device
+    double *x_in = nullptr, *x_out = nullptr, *x_temps = nullptr;  // device; x_in [2][local], x_out [2][R] by round parity
+    long long *x_bar = nullptr;   // device: the entry barrier's and the failure vote's word (multi-rank)
     unsigned long long *x_rdy = nullptr, *x_gdone = nullptr;       // device
     unsigned long long *x_ready = nullptr;                         // signal memory (or pinned, host trigger)
     bool x_ready_pinned = false;
@@ -938,12 +939,13 @@ namespace {
 
 void exchange_free(td_rounds *r) {
     for (void *p : {(void *)r->x_in, (void *)r->x_out, (void *)r->x_temps, (void *)r->x_rdy, (void *)r->x_gdone,
-                    (void *)r->x_lev, (void *)r->x_desc})
+                    (void *)r->x_lev, (void *)r->x_desc, (void *)r->x_bar})
         if (p) (void)hipFree(p);
     if (r->x_ready) (void)(r->x_ready_pinned ? hipHostFree(r->x_ready) : hipFree(r->x_ready));
     for (void *p : {(void *)r->x_log_phi, (void *)r->x_log_lev, (void *)r->x_log_t, (void *)r->x_err})
         if (p) (void)hipHostFree(p);
     r->x_in = r->x_out = r->x_temps = nullptr;
+    r->x_bar = nullptr;
     r->x_rdy = r->x_gdone = r->x_ready = nullptr;
     r->x_lev = nullptr;
     r->x_desc = nullptr;
@@ -971,8 +973,11 @@ int exchange_alloc(td_rounds *r, int R, int64_t M) {
     const int local = (int)r->chains.size();
     if (r->x_R != R) {
         exchange_free(r);
-        TD_HIP(c, hipMalloc(&r->x_in, sizeof(double) * (size_t)local));
-        TD_HIP(c, hipMalloc(&r->x_out, sizeof(double) * (size_t)R));
+        // double-buffered by round parity: a workgroup still reading round j's gathered phis cannot see a
+        // faster one's round j+1 phi (on one rank x_out is x_in)
+        TD_HIP(c, hipMalloc(&r->x_in, sizeof(double) * 2 * (size_t)local));
+        TD_HIP(c, hipMalloc(&r->x_out, sizeof(double) * 2 * (size_t)R));
+        TD_HIP(c, hipMalloc(&r->x_bar, sizeof(long long)));
         TD_HIP(c, hipMalloc(&r->x_temps, sizeof(double) * (size_t)R));
         TD_HIP(c, hipMalloc(&r->x_rdy, sizeof(unsigned long long) * (size_t)local));
         TD_HIP(c, hipMalloc(&r->x_gdone, sizeof(unsigned long long)));
@@ -1005,6 +1010,19 @@ int exchange_alloc(td_rounds *r, int R, int64_t M) {
         TD_HIP(c, hipHostMalloc(&r->x_log_t, sizeof(long long) * 3 * (size_t)M, hipHostMallocMapped));
         r->x_log_cap = M;
     }
+    return TD_OK;
+}
+
+// One-word max all-reduce over the communicator, host-synchronized: with vote 0 it is a barrier (every rank
+// has reached it when it returns); *out = the maximum vote over the ranks.
+int comm_vote(td_ctx *c, td_comm *comm, long long *word, long long vote, long long *out) {
+    TD_HIP(c, hipMemcpyAsync(word, &vote, sizeof(long long), hipMemcpyHostToDevice, comm->stream));
+    const ncclResult_t nr = ncclAllReduce(word, word, 1, ncclInt64, ncclMax, comm->comm, comm->stream);
+    if (nr != ncclSuccess) return set_err(c, TD_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    long long v = 0;
+    TD_HIP(c, hipMemcpyAsync(&v, word, sizeof(long long), hipMemcpyDeviceToHost, comm->stream));
+    TD_HIP(c, hipStreamSynchronize(comm->stream));
+    if (out) *out = v;
     return TD_OK;
 }
 
@@ -1044,9 +1062,15 @@ int td_rounds_exchange(td_rounds *r, td_comm *comm, int64_t M, int64_t K, const 
     if (M == 0) return TD_OK;
     const auto t_call = std::chrono::steady_clock::now();
     TD_HIP(c, hipSetDevice(c->device));
-    servers_quiesce(nullptr);  // (ends this launch's host-posted rounds too)
-    int rc = exchange_alloc(r, (int)R, M);
+    servers_quiesce(nullptr);
+    int rc = rounds_stop(r);  // this launch's host-posted rounds, whichever thread posted them
     if (rc) return rc;
+    rc = exchange_alloc(r, (int)R, M);
+    if (rc) return rc;
+    if (comm) {  // entry barrier: every rank is here before any kernel's exchange watchdog starts
+        rc = comm_vote(c, comm, r->x_bar, 0, nullptr);
+        if (rc) return rc;
+    }
     // every chain starts at its level's temperature; the kernel's workgroups each keep all levels
     std::vector<int> lev0((size_t)local * (size_t)R);
     std::vector<int64_t> iter0((size_t)local);
@@ -1111,12 +1135,21 @@ int td_rounds_exchange(td_rounds *r, td_comm *comm, int64_t M, int64_t K, const 
                         stuck = true;
                         break;
                     }
-                if (stuck) break;
+                if (stuck) {  // still post this rank's remaining allgathers, so that no peer waits on them forever
+                    for (int64_t q = j; q < M; ++q) {
+                        const ncclResult_t nq = ncclAllGather(r->x_in + (q & 1) * local, r->x_out + (q & 1) * R,
+                                                              (size_t)local, ncclFloat64, comm->comm, comm->stream);
+                        if (nq != ncclSuccess)
+                            return set_err(c, TD_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(nq));
+                    }
+                    break;
+                }
             } else {
                 e = hipStreamWaitValue64(comm->stream, r->x_ready, tag, hipStreamWaitValueGte);
                 if (e != hipSuccess) return hip_err(c, e, "hipStreamWaitValue64");
             }
-            const ncclResult_t nr = ncclAllGather(r->x_in, r->x_out, (size_t)local, ncclFloat64, comm->comm, comm->stream);
+            const ncclResult_t nr = ncclAllGather(r->x_in + (j & 1) * local, r->x_out + (j & 1) * R, (size_t)local,
+                                                  ncclFloat64, comm->comm, comm->stream);
             if (nr != ncclSuccess) return set_err(c, TD_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
             e = hipStreamWriteValue64(comm->stream, r->x_gdone, r->x_gtag + (unsigned long long)j + 1ull, 0);
             if (e != hipSuccess) return hip_err(c, e, "hipStreamWriteValue64");
@@ -1125,7 +1158,7 @@ int td_rounds_exchange(td_rounds *r, td_comm *comm, int64_t M, int64_t K, const 
     const auto t_enqueued = std::chrono::steady_clock::now();
     e = hipStreamSynchronize(r->stream);  // (the kernel gives up after 10 s without an exchange)
     if (e != hipSuccess) return hip_err(c, e, "exchange rounds");
-    const bool failed = *reinterpret_cast<volatile long long *>(r->x_err) != 0 || stuck;
+    bool failed = *reinterpret_cast<volatile long long *>(r->x_err) != 0 || stuck;
     if (comm) {
         if (failed && !r->x_ready_pinned) {  // release the exchange stream's waits, then drain it
             e = hipStreamWriteValue64(r->stream, r->x_ready, ~0ull >> 1, 0);
@@ -1133,6 +1166,11 @@ int td_rounds_exchange(td_rounds *r, td_comm *comm, int64_t M, int64_t K, const 
         }
         e = hipStreamSynchronize(comm->stream);
         if (e != hipSuccess) return hip_err(c, e, "exchange stream");
+        // the ranks agree on the outcome: levels are committed only when no rank failed
+        long long any = 0;
+        rc = comm_vote(c, comm, r->x_bar, failed ? 1 : 0, &any);
+        if (rc) return rc;
+        failed = any != 0;
     }
     const auto t_done = std::chrono::steady_clock::now();
     for (int k = 0; k < local; ++k) {
@@ -1142,7 +1180,7 @@ int td_rounds_exchange(td_rounds *r, td_comm *comm, int64_t M, int64_t K, const 
     }
     if (failed) {
         exchange_free(r);  // (fresh flags next time)
-        return set_err(c, TD_ERR_HIP, "td_rounds_exchange: an exchange never came (10 s)");
+        return set_err(c, TD_ERR_HIP, "td_rounds_exchange: an exchange never came (10 s) on this or another rank");
     }
     // the host replays every round's decisions on the logged phis: the device's levels must be its
     std::vector<int64_t> lv(levels, levels + R), nl((size_t)R);

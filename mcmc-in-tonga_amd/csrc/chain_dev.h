@@ -210,8 +210,8 @@ struct RoundBox {
 // every workgroup makes the same swap decisions (chain_logic.h swap_accept)
 // and takes its chain's new temperature.  Device memory except the logs.
 struct RoundX {
-    double *xin;                        // [local] this rank's phis of the round
-    const double *xout;                 // [R] every replica's phi (== xin on one rank)
+    double *xin;                        // [2][local] this rank's phis of round j in row j & 1
+    const double *xout;                 // [2][R] every replica's phi, row j & 1 (== xin on one rank)
     unsigned long long *rdy;            // [local] base + j + 1 once workgroup b's phi of round j is in xin
     unsigned long long *ready;          // base + j + 1 once all of this rank's are (workgroup 0; signal memory)
     const unsigned long long *gdone;    // base + j + 1 after round j's allgather (null on one rank)

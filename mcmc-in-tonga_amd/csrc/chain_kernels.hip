@@ -830,7 +830,7 @@ __device__ void round_exchange(const RoundX &x, int b, long long j, Shared &sh, 
     const unsigned long long tag = x.ready_base + (unsigned long long)j + 1ull;
     if (b == 0 && lane == 0) x.log_t[3 * j] = (long long)wall_clock64();
     if (lane == 0) {  // phi acknowledged before the flag (the readers load the flag, then phi)
-        mb_store(reinterpret_cast<long long *>(&x.xin[b]), __double_as_longlong(phi));
+        mb_store(reinterpret_cast<long long *>(&x.xin[(j & 1) * x.local + b]), __double_as_longlong(phi));
         __builtin_amdgcn_s_waitcnt(0);
         mb_store(reinterpret_cast<long long *>(&x.rdy[b]), (long long)tag);
     }
@@ -875,7 +875,8 @@ __device__ void round_exchange(const RoundX &x, int b, long long j, Shared &sh, 
     if (b == 0 && lane == 0) x.log_t[3 * j + 2] = (long long)wall_clock64();
     // every replica's phi and level (system-scope loads: the gathered vector bypasses the L2s)
     const bool in = lane < R;
-    const double ph = in ? __longlong_as_double(mb_load(reinterpret_cast<const long long *>(&x.xout[lane]))) : 0.0;
+    const double ph =
+        in ? __longlong_as_double(mb_load(reinterpret_cast<const long long *>(&x.xout[(j & 1) * R + lane]))) : 0.0;
     const int lv = in ? x.lev[b * R + lane] : lane;
     // owner of level l (lane l): the replica at that level -- a forward permute of the levels
     const int owner = __builtin_amdgcn_ds_permute(lv * 4, lane);

@@ -216,8 +216,10 @@ class TemperingLadder:
                                             for c in self.chains)
         # DEVICE td_chain replicas of one context: one launch resident across the rounds (td_rounds),
         # the temperatures posted to it every round instead of a launch per round.  The launch spins
-        # between rounds on a hardware queue of its own (a CU-masked stream, chain.cpp td_rounds_create),
-        # so a GPU collective's kernels (RCCL) are not held back behind it.
+        # between rounds on a high-priority non-blocking stream (comm.cpp dedicated_stream), whose
+        # hardware queue nothing else of ours uses, so a GPU collective's kernels (RCCL) are not held
+        # back behind it.  The td_comm exchange stream shares that priority pool (GPU_MAX_HW_QUEUES = 4
+        # queues per process), so a process holds only a few such streams.
         self.resident = bool(resident) and self.local >= 1 and all(
             hasattr(c, "h") and getattr(c, "ctx", None) is self.chains[0].ctx and
             getattr(getattr(c, "params", None), "engine", None) == 0 for c in self.chains)

@@ -147,3 +147,40 @@ def evaluate(rayX, rayY, rayZ, rayL, rayU, tS, allSig, cells, debug_prior=0):
                                _p(zc), _p(ze), len(xc), int(debug_prior), _p(ptS), ctypes.byref(phi),
                                ctypes.byref(lk), _p(nearest, _pi32))
     return dict(ptS=ptS, phi=phi.value, likelihood=lk.value, nearest=nearest[:P], rc=rc)
+
+
+def evaluate_threaded(rayX, rayY, rayZ, rayL, rayU, tS, allSig, cells, threads=None):
+    """MCsub.jl:123-185 for geometries too large for one core (config 5:
+    584k points x 20k cells): the rays are split into contiguous ranges, each
+    range's ptS and nearest cells come from `evaluate` on that range in its own
+    thread (ctypes releases the GIL), and phi / likelihood are the C oracle's
+    chi2 / likelihood over all rays in k order.  Identical to `evaluate` on
+    the whole geometry: a ray's t* depends on that ray alone (MCsub.jl:142-163)
+    and the chi^2 is the same sequential sum (MCsub.jl:169-173)."""
+    import threading
+
+    n = rayX.shape[1]
+    if threads is None:
+        try:
+            threads = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            threads = os.cpu_count() or 1
+        threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    threads = max(1, min(threads, n))
+    bounds = [(n * k // threads, n * (k + 1) // threads) for k in range(threads)]
+    parts = [None] * threads
+
+    def work(k):
+        a, b = bounds[k]
+        parts[k] = evaluate(rayX[:, a:b], rayY[:, a:b], rayZ[:, a:b], rayL[:, a:b], rayU[:, a:b], tS[a:b],
+                            allSig[a:b], cells)
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    ptS = np.concatenate([p["ptS"] for p in parts])
+    nearest = np.concatenate([p["nearest"] for p in parts])
+    rc = max(p["rc"] for p in parts)
+    return dict(ptS=ptS, phi=chi2(ptS, tS, allSig), likelihood=likelihood(allSig), nearest=nearest, rc=rc)

@@ -19,8 +19,10 @@ MCsub.jl:123-185) and against from-scratch evaluates of the chain's model.
 
 The end states are also checked against the C oracle (oracle/tstar_oracle.c,
 a scalar restatement of MCsub.jl:123-185), not only against another HIP path:
-the 125k-proposal config-3 chain, 4 of the 256 batch chains, and a stress
-chain on a 1500-ray subset of the config-5 rays at 3000 cells.
+the 125k-proposal config-3 chain, 4 of the 256 batch chains, the full-size
+stress chain (10k rays x 20k cells; oracle.evaluate_threaded splits its rays
+over the host cores) and a stress chain on a 1500-ray subset of the config-5
+rays at 3000 cells.
 """
 import numpy as np
 import pytest
@@ -149,7 +151,7 @@ def test_many_chains_two_per_cu_follow_solo(tt, ds, ctx, knob):
 
 
 @pytest.mark.timeout(600)
-def test_stress_chain_run_follows_host(tt):
+def test_stress_chain_run_follows_host(tt, orc):
     ds = tt.synthetic_rays(10000, seed=5)
     c = tt.TdContext.from_datastruct(ds)
     c.set_incremental(c.INCR_FULL)
@@ -164,6 +166,10 @@ def test_stress_chain_run_follows_host(tt):
     m = state_is_full_evaluate(c, dev)
     assert same_models(m, host.model())
     assert sum(st["accepted"]) > 500
+    # the end state against the C oracle at full size (rays split over the host cores)
+    ref = orc.evaluate_threaded(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig, m.cells())
+    assert ref["rc"] == 0 and ref["phi"] == m.phi == dev.stats()["phi"]
+    assert np.array_equal(ref["ptS"], m.ptS)
     dev.close()
     host.close()
     c.close()

@@ -19,21 +19,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.timeout(420)
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("launcher", ["torchrun", "none"])
+def test_bench_two_ranks_gloo(launcher):
+    """launcher "none": plain `bench.py --gpus 2`, which starts its two ranks
+    itself before any GPU call (bench.spawn_ranks)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ, TD_BENCH_BACKEND="gloo", TD_BENCH_DEVICE="0")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(TD_BENCH_BACKEND="gloo", TD_BENCH_DEVICE="0")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+    pre = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+            "127.0.0.1", "--master-port", str(port)] if launcher == "torchrun" else [sys.executable])
+    cmd = pre + [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
            "--warmup", "0", "--iters-per-step", "500", "--no-cpu-baseline", "--no-full-evaluate", "--no-dropin",
            "--batch-chains", "0", "--config4-rounds", "40", "--stress-iters", "100", "--no-phases"]
     p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=400, cwd=ROOT)
     text = p.stdout.decode(errors="replace")
     assert p.returncode == 0, text[-4000:]
-    line = [x for x in text.splitlines() if x.startswith("{")][-1]
+    lines = [x for x in text.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, text[-4000:]  # rank 0 alone prints
+    line = lines[0]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["roofline"]["bound"] == "latency"
     c4 = out["config4_ranks"]

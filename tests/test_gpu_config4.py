@@ -80,6 +80,17 @@ def test_config4_ladder_device_matches_host(tt, ctx, device_run):
     assert sorted(device_run["trace"][-1][1]) == list(range(NREP))
 
 
+def test_config4_end_states_match_oracle(orc, ds, device_run):
+    """The 8 replicas' end states after the bench's 320 rounds (3200
+    proposals each, at their ladder temperatures): (ptS, phi) of each final
+    model == the C oracle's evaluate of it, bit for bit (MCsub.jl:123-185)."""
+    for m, st in zip(device_run["models"], device_run["stats"]):
+        ref = orc.evaluate(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig, m.cells())
+        assert ref["rc"] == 0
+        assert ref["phi"] == m.phi == st["phi"]
+        assert np.array_equal(ref["ptS"], m.ptS)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

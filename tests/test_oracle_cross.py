@@ -113,3 +113,16 @@ def test_debug_prior_returns_one(tt, orc, ds):
     ref = orc.evaluate(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig,
                        tt.random_model(10, 1).cells(), debug_prior=1)
     assert ref["phi"] == 1.0 and ref["likelihood"] == 1.0
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_threaded_oracle_equals_whole_evaluate(tt, orc, ds, threads):
+    """oracle.evaluate_threaded (the checker of config 5 at full size) is the
+    whole-geometry evaluate bit for bit: per-ray t* in ray ranges, then the
+    sequential chi^2 over all rays (MCsub.jl:142-173)."""
+    cells = tt.random_model(300, 11).cells()
+    a = orc.evaluate(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig, cells)
+    b = orc.evaluate_threaded(ds.rayX, ds.rayY, ds.rayZ, ds.rayL, ds.rayU, ds.tS, ds.allSig, cells, threads=threads)
+    assert a["rc"] == b["rc"] == 0
+    assert np.array_equal(a["nearest"], b["nearest"]) and np.array_equal(a["ptS"], b["ptS"])
+    assert a["phi"] == b["phi"] and a["likelihood"] == b["likelihood"]
