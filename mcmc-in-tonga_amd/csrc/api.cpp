@@ -112,6 +112,11 @@ CellGrid make_cell_grid(const double lo[3], const double hi[3], double target, i
     }
     CellGrid G{};
     G.gx = g[0]; G.gy = g[1]; G.gz = g[2];
+    for (int a = 0; a < 3; ++a) {  // (the callers' boxes hold every cell: sealed; the shadow chain unseals)
+        G.lo[a] = lo[a];
+        G.hi[a] = hi[a];
+    }
+    G.sealed = 1;
     G.x0 = lo[0]; G.y0 = lo[1]; G.z0 = lo[2];
     double *inv[3] = {&G.ix, &G.iy, &G.iz}, *h[3] = {&G.hx, &G.hy, &G.hz}, *e[3] = {&G.ex, &G.ey, &G.ez};
     for (int a = 0; a < 3; ++a) {

@@ -364,7 +364,19 @@ int device_setup(td_chain *ch) {
         }
     const int cap = std::max<int>(ch->prm.max_cells, (int)ch->x.size()) + 1;
     // ---- bucket grid over the cells: ~2 cells per bucket at the starting size ----
-    const double glo[3] = {ch->P.xmin, ch->P.ymin, ch->P.zmin}, ghi[3] = {ch->P.xmax, ch->P.ymax, ch->P.zmax};
+    // the prior box (every valid birth and move stays in it, TD_inversion_function.jl:77-80,226-232) and the
+    // starting cells: the grid is sealed -- no cell ever lies outside it (internal.h grid_block_lb)
+    double glo[3] = {ch->P.xmin, ch->P.ymin, ch->P.zmin}, ghi[3] = {ch->P.xmax, ch->P.ymax, ch->P.zmax};
+    {
+        const std::vector<double> *cv[3] = {&ch->x, &ch->y, &ch->z};
+        for (int a = 0; a < 3; ++a) {
+            for (double v : *cv[a])
+                if (v == v) glo[a] = std::min(glo[a], v), ghi[a] = std::max(ghi[a], v);
+            const double pad = std::ldexp(std::fabs(glo[a]) + std::fabs(ghi[a]) + 1.0, -40);  // a birth's rounding
+            glo[a] -= pad;
+            ghi[a] += pad;
+        }
+    }
     const CellGrid G = make_cell_grid(glo, ghi, std::max<double>((double)ch->x.size(), 16.0) / 2.0, 256, 1 << 24);
     const size_t nbuckets = (size_t)G.gx * G.gy * G.gz;
     std::vector<int> bcount(nbuckets, 0);
@@ -387,7 +399,7 @@ int device_setup(td_chain *ch) {
     add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * (ntiles + 1)); add(sizeof(int) * Pn);
     add(sizeof(float) * 3 * ntiles); add(sizeof(float) * 3 * ntiles); add(sizeof(double) * (ntiles + 1)); add(sizeof(double) * (ntiles + 1));
     add(sizeof(float) * 3 * std::max(nsuper, 1)); add(sizeof(float) * 3 * std::max(nsuper, 1));
-    add(sizeof(double) * 4 * cap); add(sizeof(double) * (cap + 2)); for (int i = 0; i < 4; ++i) add(sizeof(int) * cap);
+    add(sizeof(double) * 4 * cap); add(sizeof(double) * (cap + 2)); for (int i = 0; i < 3; ++i) add(sizeof(int) * cap); add(sizeof(long long) * cap);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn);
     add(sizeof(int) * Pn); add(sizeof(double) * Pn); add(sizeof(double) * Pn); add(Pn);
     add(sizeof(int) * Pn); add(sizeof(int) * Pn); add(sizeof(int) * (ntiles + 1));
@@ -421,7 +433,7 @@ int device_setup(td_chain *ch) {
     d.cx = cells; d.cy = cells + cap; d.cz = cells + 2 * cap; d.czeta = cells + 3 * cap;
     double *logN_d = carve<double>(cur, (size_t)cap + 2);
     d.logN = logN_d;
-    d.order = carve<int>(cur, cap); d.rank = carve<int>(cur, cap);
+    d.order = carve<int>(cur, cap); d.stamp = carve<long long>(cur, cap);
     d.free_slots = carve<int>(cur, cap); d.order_tmp = carve<int>(cur, cap);
     d.cap = cap;
     d.best_s = carve<int>(cur, Pn); d.best_d = carve<double>(cur, Pn); d.zeta0 = carve<double>(cur, Pn);
@@ -451,7 +463,8 @@ int device_setup(td_chain *ch) {
     if (e != hipSuccess) return hip_err(c, e, "hipHostGetDevicePointer(chain scalars)");
     // ---- uploads ----
     const int N = (int)ch->x.size();
-    std::vector<int> ident((size_t)cap), rank0((size_t)cap, -1);  // slots >= N are free
+    std::vector<int> ident((size_t)cap);
+    std::vector<long long> rank0((size_t)cap, -1);  // stamps: slots >= N are free
     for (int i = 0; i < cap; ++i) ident[(size_t)i] = i;
     for (int i = 0; i < N; ++i) rank0[(size_t)i] = i;
     std::vector<double> hc(4 * (size_t)cap, 0.0);
@@ -464,6 +477,7 @@ int device_setup(td_chain *ch) {
     s0.ncells = N;
     s0.nslots = N;
     s0.nfree = 0;
+    s0.next_stamp = N;  // stamps 0..N-1: the starting cells in Julia order
     s0.phi = 1.0;  // debug_prior: evaluate returns phi = 1 (MCsub.jl:131)
     std::vector<double> logN((size_t)cap + 2);  // logN[k] = det_log(k): the MH model-size factor
     for (size_t k = 0; k < logN.size(); ++k) logN[k] = tdchain::det_log((double)k);
@@ -478,7 +492,7 @@ int device_setup(td_chain *ch) {
         {shi_d, shi.data(), sizeof(float) * shi.size()},
         {cells, hc.data(), sizeof(double) * hc.size()},
         {d.order, ident.data(), sizeof(int) * (size_t)cap},
-        {d.rank, rank0.data(), sizeof(int) * (size_t)cap},
+        {d.stamp, rank0.data(), sizeof(long long) * (size_t)cap},
         {d.bucket_count, bcount.data(), sizeof(int) * nbuckets},
         {d.buckets, bent.data(), sizeof(CellEntry) * bent.size()},
         {d.bslot, bslot.data(), sizeof(int) * bslot.size()},
@@ -1479,6 +1493,8 @@ int shadow_chain_create(td_ctx *ctx, const double *x, const double *y, const dou
     td_chain *ch = nullptr;
     int rc = td_chain_create(&ch, ctx, &p, x, y, z, zeta, ncells);
     if (rc) return rc;
+    ch->dev.grid.sealed = 0;  // the caller's edits may put a cell anywhere: bounds from the faces only
+    ch->desc_dirty = true;
     hipError_t e = hipHostMalloc(&ch->script_host, sizeof(double) * ((size_t)ctx->g.n + 2),
                                  hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&ch->script_dev), ch->script_host, 0);

@@ -1,8 +1,11 @@
 // chain_dev.h -- device state of one rj-MCMC chain (TD_ENGINE_DEVICE).
 //
-// Cells live in SLOTS (stable storage); order[pos] = slot and rank[slot] =
-// pos keep the Julia order (birth appends, death deleteat!-shifts), which
-// decides nearest-cell ties.  Per ray point the chain caches the exact FP64
+// Cells live in SLOTS (stable storage); order[pos] = slot keeps the Julia
+// order (birth appends, death deleteat!-shifts), which decides nearest-cell
+// ties.  Ties compare STAMPS: stamp[slot] = the order the cell entered the
+// model (the starting cells 0..N-1, each birth the next number), which is
+// Julia position order -- a birth appends after every live cell, a death
+// keeps the others' order -- so a death rewrites no per-slot number.  Per ray point the chain caches the exact FP64
 // (slot, squared distance, zeta) of its nearest cell -- exactly what a full
 // v_nearest scan would give -- so a proposal only touches:
 //   birth : points the new cell captures (d < cached d)
@@ -56,6 +59,7 @@ struct ChainScalars {
     int last_action;       // Model.action / Model.accept of the last iteration (TD_inversion_function.jl:73-74,
     int last_accept;       // 123,179,217,249): the proposal drawn and whether it was accepted
     int pad;
+    int64_t next_stamp;    // the next birth's stamp (64-bit: never wraps)
 };
 
 // A proposal given by the host instead of drawn (td_evaluate's incremental
@@ -94,7 +98,8 @@ struct DevChain {
     // cells by slot
     double *cx, *cy, *cz, *czeta;  // [cap]
     const double *logN;            // [cap+2] det_log(k), the MH model-size factor
-    int *order, *rank, *free_slots, *order_tmp;  // [cap]
+    int *order, *free_slots, *order_tmp;  // [cap]
+    long long *stamp;                     // [cap]; -1 = a free slot
     int cap;
     // per-point cache (current state) and candidate overlay
     int *best_s;

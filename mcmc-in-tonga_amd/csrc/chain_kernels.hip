@@ -82,7 +82,8 @@ __device__ __forceinline__ double dist2(double cx, double cy, double cz, double 
 
 // (distance, Julia position) lexicographic order; a cell must also beat the
 // 1e9 sentinel strictly (MCsub.jl:250,255).
-__device__ __forceinline__ bool better(double d, int r, double bd, int br) {
+template <class R>
+__device__ __forceinline__ bool better(double d, R r, double bd, R br) {
     return d < bd || (d == bd && d < kSentinel && r < br);
 }
 
@@ -222,6 +223,7 @@ struct Shared {
     long long proposed[5], accepted[5];
     double phi;
     int ncells, nslots, nfree;
+    long long next_stamp;  // the next birth's stamp (tid 0)
     double lnN[3];     // logN[ncells - 1 .. ncells + 1]
     double lnN_far[2];  // logN[ncells - 2], logN[ncells + 2]: read during phase F for a birth/death commit
     double q_zeta;         // result of the birth/death Interpolation query
@@ -244,7 +246,22 @@ struct Shared {
     // terr; a proposal adds dsum = its terms' changes (any order), dabs = their magnitudes (phase E)
     double tsum, terr, dsum, dabs, b_T, b_E;
     double wpart[kChainThreads / 64];  // each wave's part of a block-wide any-order sum of the terms
+    // a death, rays in LDS, free-running: phase G's deleteat! shift (shift_range) by waves 1.. -- each
+    // wave's last source read in phase F (shift_edge), the waves done counted in shift_done, which wave 0
+    // waits for before it reads the order for the next proposal
+    int shift_done;
+    int shift_edge[kChainThreads / 64];
 };
+
+// deleteat! at Julia position `index` (rays in LDS, free-running): positions index+1 .. ncells-1 move down
+// one, wave w (1 .. nw) taking the source positions [a, b).  Each wave reads its sources and writes
+// them one lower in passes of 64 (a pass reads before it writes); the one source another wave writes
+// over -- position b-1, the next wave's first target -- was read in phase F (Shared::shift_edge).
+__device__ __forceinline__ void shift_range(int index, int ncells, int w, int nw, int &a, int &b) {
+    const int first = index + 1, C = (ncells - first + nw - 1) / nw;
+    a = first + (w - 1) * C;
+    b = min(a + C, ncells);
+}
 
 // Diagnostic phase stamp (lane 0 of wave 0, right after a barrier): cycles
 // since the previous stamp are charged to phase k.  Off unless d.profile.
@@ -371,8 +388,10 @@ struct Nearest {
 
 // Exact nearest live cell by scanning every slot, ONE wave: lexicographic
 // (distance, Julia position), which is what v_nearest's first-index rule
-// gives (MCsub.jl:250-258).  Fallback of the grid search (rare: out of line).
-__device__ __attribute__((noinline)) Nearest wave_full_scan(const int *__restrict__ rank, const int *ord,
+// gives (MCsub.jl:250-258) -- positions compared through the slots' stamps,
+// which are in Julia order (chain_dev.h).  Fallback of the grid search (rare:
+// out of line).
+__device__ __attribute__((noinline)) Nearest wave_full_scan(const long long *__restrict__ stamp,
                                                            const double *__restrict__ cx,
                                                            const double *__restrict__ cy,
                                                            const double *__restrict__ cz,
@@ -380,16 +399,17 @@ __device__ __attribute__((noinline)) Nearest wave_full_scan(const int *__restric
                                                            int lane, double x, double y, double z, int skip,
                                                            int moved, double mx, double my, double mz) {
     double bd = kSentinel;
-    int br = INT_MAX;
+    long long br = LLONG_MAX;
+    int bs = -1;
     constexpr int kScanUnroll = 8;  // all loads of a round issued before any use
     for (int s0 = lane; s0 < nslots; s0 += kScanUnroll * 64) {
-        int r[kScanUnroll];
+        long long r[kScanUnroll];
         double px[kScanUnroll], py[kScanUnroll], pz[kScanUnroll];
 #pragma unroll
         for (int u = 0; u < kScanUnroll; ++u) {
             // unconditional loads from a clamped slot, masked afterwards
             const int s = min(s0 + u * 64, cap - 1);
-            r[u] = rank[s];
+            r[u] = stamp[s];
             px[u] = cx[s];
             py[u] = cy[s];
             pz[u] = cz[s];
@@ -407,18 +427,20 @@ __device__ __attribute__((noinline)) Nearest wave_full_scan(const int *__restric
             if (better(dd, r[u], bd, br)) {
                 bd = dd;
                 br = r[u];
+                bs = s;
             }
         }
     }
     // lexicographic min: the distance first, then the position among equals
     const unsigned long long kd = wave_min_u64((unsigned long long)__double_as_longlong(bd));
     const bool at_min = (unsigned long long)__double_as_longlong(bd) == kd;
-    const unsigned long long kr = wave_min_u64(at_min ? (unsigned long long)(unsigned)br : ~0ull);
+    const unsigned long long kr = wave_min_u64(at_min ? (unsigned long long)br : ~0ull);
     Nearest res;
     res.d = __longlong_as_double((long long)kd);
     res.proven = true;
-    if (res.d < kSentinel && kr != ~0ull) {
-        res.s = ord[(int)kr];
+    if (res.d < kSentinel && kr != ~0ull) {  // (stamps are unique: one lane holds the winner)
+        const unsigned long long who = __ballot(at_min && (unsigned long long)br == kr);
+        res.s = __builtin_amdgcn_readlane(bs, __builtin_ctzll(who));
         res.z = czeta[res.s];
     } else {
         res.s = -1;
@@ -507,7 +529,7 @@ __device__ __forceinline__ Nearest wave_nearest(const DevChain &d, const Views &
     Nearest r = wave_grid_search(d, sh.grid_ovf != 0, lane, x, y, z, skip, moved, mx, my, mz, mzeta);
     if (!r.proven) {
         if (lane == 0) atomicAdd(&sh.grid_fallbacks32, 1);
-        r = wave_full_scan(d.rank, v.ord, d.cx, d.cy, d.cz, d.czeta, d.cap, sh.nslots, lane, x, y, z, skip, moved,
+        r = wave_full_scan(d.stamp, d.cx, d.cy, d.cz, d.czeta, d.cap, sh.nslots, lane, x, y, z, skip, moved,
                            mx, my, mz);
     }
     return r;
@@ -1122,6 +1144,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         for (int k = 0; k < 3; ++k) sh.lnN[k] = d.logN[max(s0.ncells - 1 + k, 0)];
         sh.nslots = s0.nslots;
         sh.nfree = s0.nfree;
+        sh.next_stamp = s0.next_stamp;
         sh.g_op = 0;
         sh.grid_ovf = *d.grid_overflow;
         sh.rT = P.temperature;
@@ -1437,7 +1460,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                     }
             }
-            if (RLDS && action == tdchain::kDeath) {  // deleteat! shift, staged before we know if it is accepted
+            if (RLDS && action == tdchain::kDeath && nscript) {  // deleteat! shift, staged before we know if it is accepted
                 const int sthr = query ? NTH - 64 : NTH;  // not the query wave: it starts at once
                 // (the order in HBM: no staging -- an accepted death shifts it in phase G)
                 if constexpr (RLDS) {
@@ -1467,9 +1490,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 // ================= phase C: affected points =================
 
                 const int nt = sh.n_tiles;
-                // the selected cell's Julia position and value, known since the proposal was made:
-                // rank[slot_k] = p.index (slot_k = ord[p.index]), czeta[slot_k] = zeta_killed (no load)
-                const int rank_k = slot_k >= 0 ? (int)p.index : 0;
+                // the selected cell's value, known since the proposal was made: czeta[slot_k] = zeta_killed
                 const double zeta_k = slot_k >= 0 ? zeta_killed : 0.0;
                 int seen = 0;
                 // one candidate point: captured (birth, move), re-valued (change) or orphaned
@@ -1486,7 +1507,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         if (o < kOrphanLds) sh.orph[o] = OrphanRec{qx, qy, qz, q, ray};
                     } else if (action == tdchain::kMove) {
                         const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
-                        if (dd < bd || (dd == bd && s >= 0 && rank_k < d.rank[s]))
+                        // (an exact tie: Julia positions, through the stamps -- loaded only then)
+                        if (dd < bd || (dd == bd && s >= 0 && d.stamp[slot_k] < d.stamp[s]))
                             mark(d, v, sh, q, ray, slot_k, dd, zeta_k);
                     }
                 };
@@ -1655,19 +1677,26 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                     if (!act || part != 0) continue;
                                     // every cell outside the region lies beyond one of its inner faces
                                     double lb = __builtin_huge_val();
-                                    auto face = [&lb](double w, double w0, double h, double e, int g, int lo, int hi) {
+                                    // (and, the grid sealed, its distance to the cells' box: internal.h grid_block_lb)
+                                    double o2[3];
+                                    grid_out2(G, qx, qy, qz, o2);
+                                    auto face = [&lb](double w, double w0, double h, double e, int g, int lo, int hi,
+                                                      double other) {
                                         if (lo > 0) {
                                             const double gap = (w - (w0 + (double)lo * h)) - e;
-                                            lb = gap > 0.0 ? (gap * gap < lb ? gap * gap : lb) : 0.0;
+                                            const double f = (gap > 0.0 ? gap * gap : 0.0) + other;
+                                            lb = f < lb ? f : lb;
                                         }
                                         if (hi < g - 1) {
                                             const double gap = ((w0 + (double)(hi + 1) * h) - w) - e;
-                                            lb = gap > 0.0 ? (gap * gap < lb ? gap * gap : lb) : 0.0;
+                                            const double f = (gap > 0.0 ? gap * gap : 0.0) + other;
+                                            lb = f < lb ? f : lb;
                                         }
                                     };
-                                    face(qx, G.x0, G.hx, G.ex, G.gx, i0, i1);
-                                    face(qy, G.y0, G.hy, G.ey, G.gy, j0, j1);
-                                    face(qz, G.z0, G.hz, G.ez, G.gz, k0b, k1b);
+                                    face(qx, G.x0, G.hx, G.ex, G.gx, i0, i1, o2[1] + o2[2]);
+                                    face(qy, G.y0, G.hy, G.ey, G.gy, j0, j1, o2[0] + o2[2]);
+                                    face(qz, G.z0, G.hz, G.ez, G.gz, k0b, k1b, o2[0] + o2[1]);
+                                    lb = grid_lb_close(lb);
                                     if (bs >= 0 && bd < kSentinel && !tie && bd < lb) {
                                         const int q = o < kOrphanLds ? sh.orph[o].q : d.orphans[o];
                                         const int ray = o < kOrphanLds ? sh.orph[o].ray : d.pt_ray[q];
@@ -1836,6 +1865,15 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     const double wsum = wave_sum_f64((p0 + p1) + (p2 + p3));
                     if (lane == 0) sh.wpart[wv] = wsum;
                     __syncthreads();
+                }
+            }
+            if (RLDS && !nscript && action == tdchain::kDeath && lane == 0) {  // what phase G's shift overwrites
+                if (wv != 0) {
+                    int a, b;
+                    shift_range((int)p.index, ncells, wv, kWv - 1, a, b);
+                    if (b > a) sh.shift_edge[wv] = v.ord[b - 1];
+                } else {
+                    sh.shift_done = 0;
                 }
             }
             if (wv == 0) {
@@ -2106,7 +2144,25 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     pend_r = true;  // written at the top of the next iteration
                     if (wv == 1) delta_remark(v.term, v.prefix, v.cprefix, n, sh.dseg, smask, lane);
                 }
-                if (RLDS && action == tdchain::kDeath && wv != 0) {  // deleteat!: positions after the killed one shift down
+                if (RLDS && action == tdchain::kDeath && wv != 0 && !nscript) {  // deleteat!, in LDS (shift_range)
+                    int a, b;
+                    shift_range((int)pp.index, ncells, wv, kWv - 1, a, b);
+                    if (b > a) {
+                        const int edge = sh.shift_edge[wv];
+                        for (int j0 = a; j0 < b; j0 += 64) {
+                            const int j = j0 + lane;
+                            if (j < b) {
+                                const int sl = j == b - 1 ? edge : v.ord[j];
+                                v.ord[j - 1] = sl;
+                            }
+                        }
+                    }
+                    if (lane == 0) {  // (this wave's stores are done: the add is ordered after them)
+                        __builtin_amdgcn_s_waitcnt(0);
+                        atomicAdd(&sh.shift_done, 1);
+                    }
+                }
+                if (RLDS && action == tdchain::kDeath && wv != 0 && nscript) {  // deleteat!: from the staged copy
                     constexpr int U = 4;                                 // U loads in flight per thread
                     for (int j0 = (int)pp.index + 1 + w; j0 < ncells; j0 += U * kW) {
                         int sl[U];
@@ -2115,10 +2171,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
 #pragma unroll
                         for (int u = 0; u < U; ++u) {
                             const int j = j0 + u * kW;
-                            if (j < ncells) {
-                                v.ord[j - 1] = sl[u];
-                                d.rank[sl[u]] = j - 1;
-                            }
+                            if (j < ncells) v.ord[j - 1] = sl[u];
                         }
                     }
                 }
@@ -2132,7 +2185,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         d.cz[s] = pp.z;
                         d.czeta[s] = pp.zeta;
                         v.ord[ncells] = s;
-                        d.rank[s] = ncells;
+                        const long long st_new = sh.next_stamp;  // appended: after every live cell in Julia order
+                        d.stamp[s] = st_new;
+                        sh.next_stamp = st_new + 1;
                         if (sh.nfree > 0)
                             sh.nfree -= 1;
                         else
@@ -2145,7 +2200,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     } else if (action == tdchain::kDeath) {
                         d.free_slots[sh.nfree] = sk;
                         sh.nfree += 1;
-                        d.rank[sk] = -1;
+                        d.stamp[sk] = -1;  // a free slot
                         sh.ncells = ncells - 1;
                         const double a = sh.lnN_far[0], b = sh.lnN[0], c = sh.lnN[1];
                         sh.lnN[0] = a;
@@ -2187,10 +2242,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
 #pragma unroll
                             for (int u = 0; u < U; ++u) {
                                 const int j = b0 + tid + u * NTH;
-                                if (j < ncells) {
-                                    v.ord[j - 1] = sl[u];
-                                    d.rank[sl[u]] = j - 1;
-                                }
+                                if (j < ncells) v.ord[j - 1] = sl[u];
                             }
                         }
                         __syncthreads();
@@ -2249,11 +2301,16 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         cur_r ^= 1;  // adopt the guess: no copy
                         sh.cur = cur_r;
                     } else {
-                        // a just-killed position: later positions read the pre-shift order (LDS
-                        // layout; in the HBM order phase G has shifted it already)
-                        const int killed = (RLDS && acc && action == tdchain::kDeath) ? (int)pp.index : -1;
+                        // a just-killed position (LDS layout; in the HBM order phase G has shifted it already):
+                        // scripted steps read the staged pre-shift order; a free-running chain the order once
+                        // the shifting waves are done
+                        const bool killed = RLDS && acc && action == tdchain::kDeath;
+                        if (killed && !nscript)
+                            while (__hip_atomic_load(&sh.shift_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                                   kWv - 1)
+                                __builtin_amdgcn_s_sleep(1);
                         auto slot_at = [&](int pos) {
-                            return (killed >= 0 && pos >= killed) ? d.order_tmp[pos + 1] : v.ord[pos];
+                            return (killed && nscript && pos >= (int)pp.index) ? d.order_tmp[pos + 1] : v.ord[pos];
                         };
                         if (nscript) {
                             sh.step_cur = mb ? sh.srv_step[sh.srv_k++] : sa.step[it + 1];
@@ -2318,6 +2375,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         s.ncells = sh.ncells;
         s.nslots = sh.nslots;
         s.nfree = sh.nfree;
+        s.next_stamp = sh.next_stamp;
         if (iters > 0) {
             s.last_action = last_action;
             s.last_accept = last_accept;

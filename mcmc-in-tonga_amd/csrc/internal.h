@@ -84,6 +84,11 @@ struct CellGrid {
     // allowance for the rounding of bucket assignment against the faces
     // x0 + i*hx: a cell can sit up to ex on the wrong side of a face
     double ex, ey, ez;
+    // sealed != 0: every cell lies inside [lo, hi] on each axis (the evaluate's cells' own box; the
+    // device chain's prior box, which every valid proposal stays in) -- a query point outside that box
+    // is at least its distance to the box from every cell (grid_block_lb)
+    double lo[3], hi[3];
+    int sealed;
 };
 
 // A uniform grid with about `target` buckets over the box [lo, hi] (degenerate
@@ -110,23 +115,47 @@ __host__ __device__ inline int grid_bucket(const CellGrid &G, double x, double y
 // the grid boundary excluded (no cell lies beyond them).  Every cell outside
 // the block is at least this far away (0 when unknown; +inf when the block
 // covers the grid).
+//
+// A sealed grid also bounds by the point's distance to the cells' box: a cell
+// beyond an x face lies inside the box in y and z, so it is at least
+// sqrt(gap_x^2 + out_y^2 + out_z^2) away (out_a = the point's distance to the
+// box along a, 0 inside).  That proves the nearest cell of a point outside the
+// box (the ray ends past the prior box's y range, 3 % of the 381 rays'
+// points) from the 3x3x3 block, where the faces alone never could.
+__host__ __device__ inline void grid_out2(const CellGrid &G, double x, double y, double z, double o2[3]) {
+    const double v[3] = {x, y, z}, e[3] = {G.ex, G.ey, G.ez};
+    for (int a = 0; a < 3; ++a) {
+        double o = 0.0;
+        if (G.sealed) {
+            const double below = G.lo[a] - v[a], above = v[a] - G.hi[a];
+            o = (below > above ? below : above) - e[a];  // (NaN: not > 0)
+        }
+        o2[a] = o > 0.0 ? o * o : 0.0;
+    }
+}
+// min over faces of gap^2 + the other axes' out^2, made a strict lower bound of every FP64 dist2 beyond
+__host__ __device__ inline double grid_lb_close(double lb) { return lb * (1.0 - 0x1p-40); }
 __host__ __device__ inline double grid_block_lb(const CellGrid &G, double x, double y, double z, int R) {
     double lb = __builtin_huge_val();
-    auto face = [&lb](double v, double v0, double inv, double h, double e, int g, int R_) {
+    double o2[3];
+    grid_out2(G, x, y, z, o2);
+    auto face = [&lb](double v, double v0, double inv, double h, double e, int g, int R_, double other) {
         const int i = grid_axis(v, v0, inv, g);
         if (i - R_ > 0) {
             const double gap = (v - (v0 + (double)(i - R_) * h)) - e;
-            lb = gap > 0.0 ? (gap * gap < lb ? gap * gap : lb) : 0.0;
+            const double f = (gap > 0.0 ? gap * gap : 0.0) + other;
+            lb = f < lb ? f : lb;
         }
         if (i + R_ < g - 1) {
             const double gap = ((v0 + (double)(i + R_ + 1) * h) - v) - e;
-            lb = gap > 0.0 ? (gap * gap < lb ? gap * gap : lb) : 0.0;
+            const double f = (gap > 0.0 ? gap * gap : 0.0) + other;
+            lb = f < lb ? f : lb;
         }
     };
-    face(x, G.x0, G.ix, G.hx, G.ex, G.gx, R);
-    face(y, G.y0, G.iy, G.hy, G.ey, G.gy, R);
-    face(z, G.z0, G.iz, G.hz, G.ez, G.gz, R);
-    return lb;
+    face(x, G.x0, G.ix, G.hx, G.ex, G.gx, R, o2[1] + o2[2]);
+    face(y, G.y0, G.iy, G.hy, G.ey, G.gy, R, o2[0] + o2[2]);
+    face(z, G.z0, G.iz, G.hz, G.ez, G.gz, R, o2[0] + o2[1]);
+    return grid_lb_close(lb);
 }
 
 constexpr int kGridMaxBuckets = 1 << 16;  // bucket grid of the evaluate path
