@@ -20,11 +20,11 @@ Also reported:
                    bound is LATENCY (one persistent workgroup per chain: a
                    chain of dependent barriers and LDS/L2 round trips per
                    proposal); `latency` gives the measured phase cycles.  The
-                   HBM line beside it prices what the incremental proposals
-                   actually read (counted in-kernel: tile boxes, candidate
-                   points, grid queries, re-summed ray points, chi^2 terms)
-                   against HBM peak; the full-evaluate bytes of SURVEY 8(d)
-                   are reported only as `reference_structure_bytes_per_proposal`.
+                   HBM line prices SURVEY 8(d)'s algorithmic bytes of one
+                   evaluate per proposal against HBM peak; `incremental_*`
+                   beside it is what the incremental proposals actually read
+                   (counted in-kernel: tile boxes, candidate points, grid
+                   queries, re-summed ray points, chi^2 terms).
   full_evaluate -- the drop-in td_evaluate path (brute-force P x N nearest
                    search, MCsub.jl:123-185) on the same model: latency and
                    the FP64-VALU roofline of its dominant kernel.
@@ -81,24 +81,28 @@ def model_bytes(P, n, N):
 def chain_roofline(kernel, ref_bytes_per_proposal, proposals_per_launch, avg_launch_s, counted_bytes_per_launch,
                    traffic_key, match):
     """roofline block of a chain kernel.  bound = latency.
-    The HBM line: `achieved` = the bytes the incremental proposals read,
-    counted in-kernel (tile boxes 32 B per tested tile, 36 B per candidate
-    point, 27 x 8 x 32 B per grid query, 17 B per re-summed ray point, 28 B
-    per chi^2 term), per launch / the launch's HIP-event time; `traffic` =
-    the PMC-measured HBM bytes per launch from the committed rocprofv3
-    profile of the same command (`traffic_source`).  SURVEY 8(d)'s
-    full-evaluate bytes are what the reference's structure would read per
-    proposal: reported, never priced against the peak."""
-    achieved = counted_bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    The HBM line: `achieved` = SURVEY 8(d)'s algorithmic bytes of one
+    evaluate (24 P + 8 S + 32 N + 24 n, model_bytes) x the proposals of one
+    launch / the launch's HIP-event time -- what the reference's structure must
+    move per proposal; `traffic` = the PMC-measured HBM bytes per launch from
+    the committed rocprofv3 profile of the same command (`traffic_source`).
+    Beside them, `incremental_*`: the bytes the incremental proposals actually
+    read, counted in-kernel (tile boxes 32 B per tested tile, 36 B per
+    candidate point, 27 x 8 x 32 B per grid query, 17 B per re-summed ray
+    point, 28 B per chi^2 term)."""
+    alg = float(ref_bytes_per_proposal) * proposals_per_launch
+    achieved = alg / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    inc = counted_bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     out = {"kernel": kernel, "bound": "latency",
            "limiter": "one persistent workgroup per chain: dependent barriers and LDS/L2 round trips "
                       "(DESIGN.md 4.2); HBM line below",
            "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None, "traffic_source": None,
-           "bytes_model": "in-kernel count of what the incremental proposals read (tile boxes, candidate points, "
-                          "grid queries, re-summed ray points, chi^2 terms)",
-           "algorithmic_bytes_per_launch": round(counted_bytes_per_launch, 1),
-           "reference_structure_bytes_per_proposal": ref_bytes_per_proposal,
+           "bytes_model": "SURVEY 8(d): 24 P + 8 S + 32 N + 24 n bytes per proposal (one evaluate)",
+           "algorithmic_bytes_per_proposal": ref_bytes_per_proposal,
+           "algorithmic_bytes_per_launch": round(alg, 1),
+           "incremental_bytes_per_launch": round(counted_bytes_per_launch, 1),
+           "incremental_achieved": round(inc, 3), "incremental_frac": round(inc / HBM_PEAK_GBS, 6),
            "proposals_per_launch": proposals_per_launch, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
            "us_per_proposal": round(avg_launch_s / max(proposals_per_launch, 1) * 1e6, 4)}
     if match:

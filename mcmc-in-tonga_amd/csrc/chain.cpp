@@ -59,6 +59,14 @@ struct td_chain {
     std::chrono::steady_clock::time_point srv_last{};
     ScriptStep srv_pending{};     // the step the server holds undecided (kDecideLater), if any
     bool srv_has_pending = false;
+    // a command posted and not yet answered (shadow_server_post / shadow_server_answer)
+    bool post_open = false;
+    int post_decision = 0, post_nsteps = 0;
+    ScriptStep post_steps[kMaxScript]{};
+    ScriptStep post_held{};
+    bool post_had = false;
+    long long post_seq = 0;
+    int64_t post_t0 = 0;
     td_rounds *rounds = nullptr;  // a resident tempering launch holds this chain (td_rounds_*)
 };
 
@@ -673,14 +681,12 @@ int server_start(td_chain *ch) {
     return TD_OK;
 }
 
-// Post the command already written into the mailbox and wait for its answer.
-// kExitedEarly: the kernel had returned (idle watchdog) before it read the
-// command -- its pending proposal undone, its state written back, nothing of
-// the command done; the caller re-issues it to a new launch.
-int server_post(td_chain *ch) {
+// Wait for the answer to command `sq`.  kExitedEarly: the kernel had returned
+// (idle watchdog) before it read the command -- its pending proposal undone,
+// its state written back, nothing of the command done; the caller re-issues it
+// to a new launch.
+int server_wait(td_chain *ch, long long sq) {
     Mailbox *m = ch->mb_host;
-    const long long sq = m->seq + 1;
-    post_seq(m, sq);
     const auto t0 = std::chrono::steady_clock::now();
     for (long long spin = 0;; ++spin) {
         if (*vol(&m->done) == sq) break;
@@ -700,6 +706,7 @@ int server_post(td_chain *ch) {
     ch->srv_last = std::chrono::steady_clock::now();
     return TD_OK;
 }
+
 
 // ---- resident tempering rounds ----
 int rounds_stop(td_rounds *r) {
@@ -1596,52 +1603,79 @@ bool shadow_server_alive(td_chain *ch) {
     return true;
 }
 
-int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,
-                       double *phi_out, double *ptS_out) {
-    if (nsteps < 1 || nsteps > kMaxScript) return set_err(ch->ctx, TD_ERR_ARG, "server steps");
-    ScriptStep st[kMaxScript];
-    for (int k = 0; k < nsteps; ++k) st[k] = steps[k];
-    for (int attempt = 0;; ++attempt) {
-        int rc = server_start(ch);
-        if (rc) return rc;
-        if (attempt == 0 && g_post_delay_ms.load() > 0)
-            std::this_thread::sleep_for(std::chrono::milliseconds(g_post_delay_ms.load()));
-        Mailbox *m = ch->mb_host;
-        m->type = kCmdEval;
-        m->decision = decision;
-        m->nsteps = nsteps;
-        for (int k = 0; k < nsteps; ++k) m->step[k] = st[k];
-        const ScriptStep held = ch->srv_pending;
-        const bool had = ch->srv_has_pending;
-        const int64_t t0 = now_ns();
-        rc = server_post(ch);
-        ch->ctx->dropin_ns[2] += now_ns() - t0;
-        if (rc == TD_OK) ch->ctx->dropin_ns[16] += 10 * *vol(&ch->mb_host->diag[1]);  // (100 MHz ticks)
-        if (rc == TD_OK) {
-            ch->srv_pending = st[nsteps - 1];
-            ch->srv_has_pending = st[nsteps - 1].decision == kDecideLater;
-            break;
-        }
-        if (rc != kExitedEarly || attempt > 0) {
-            return rc == kExitedEarly ? set_err(ch->ctx, TD_ERR_HIP, "chain server returned before answering twice")
-                                      : rc;
-        }
-        // the kernel undid its pending proposal and never read this command: a fresh launch
-        // gets it again, preceded by that proposal as a committed step if the caller accepted it
-        if (decision == 1 && had) {
+// Server mode, split so the caller can work while the device evaluates: post an evaluate command
+// (its steps, the fate of the pending proposal), and later take its answer.  One command open at a time.
+namespace {
+int server_post_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, bool reissue) {
+    if (nsteps < 1 || nsteps > kMaxScript || ch->post_open) return set_err(ch->ctx, TD_ERR_ARG, "server steps");
+    int rc = server_start(ch);
+    if (rc) return rc;
+    if (!reissue && g_post_delay_ms.load() > 0)  // (testing: the host descheduled before its post)
+        std::this_thread::sleep_for(std::chrono::milliseconds(g_post_delay_ms.load()));
+    Mailbox *m = ch->mb_host;
+    m->type = kCmdEval;
+    m->decision = decision;
+    m->nsteps = nsteps;
+    for (int k = 0; k < nsteps; ++k) m->step[k] = ch->post_steps[k] = steps[k];
+    ch->post_decision = decision;
+    ch->post_nsteps = nsteps;
+    ch->post_held = ch->srv_pending;
+    ch->post_had = ch->srv_has_pending;
+    ch->post_t0 = now_ns();
+    ch->post_seq = m->seq + 1;
+    post_seq(m, ch->post_seq);
+    ch->post_open = true;
+    return TD_OK;
+}
+}  // namespace
+
+int shadow_server_post(td_chain *ch, int decision, const ScriptStep *steps, int nsteps) {
+    return server_post_eval(ch, decision, steps, nsteps, false);
+}
+
+int shadow_server_answer(td_chain *ch, const double *base_ptS, double *phi_out, double *ptS_out) {
+    if (!ch->post_open) return set_err(ch->ctx, TD_ERR_ARG, "server: no command posted");
+    ch->post_open = false;
+    int rc = server_wait(ch, ch->post_seq);
+    ch->ctx->dropin_ns[2] += now_ns() - ch->post_t0;
+    if (rc == kExitedEarly) {
+        // the kernel undid its pending proposal and never read this command: a fresh launch gets it
+        // again, preceded by that proposal as a committed step if the caller accepted it
+        ScriptStep st[kMaxScript];
+        int nsteps = ch->post_nsteps;
+        for (int k = 0; k < nsteps; ++k) st[k] = ch->post_steps[k];
+        if (ch->post_decision == 1 && ch->post_had) {
             if (nsteps + 1 > kMaxScript) return set_err(ch->ctx, TD_ERR_HIP, "chain server: lost a pending commit");
             for (int k = nsteps; k > 0; --k) st[k] = st[k - 1];
-            st[0] = held;
+            st[0] = ch->post_held;
             st[0].decision = 1;
             ++nsteps;
         }
-        decision = 0;  // nothing pending on the new launch
+        rc = server_post_eval(ch, 0, st, nsteps, true);  // (nothing pending on the new launch)
+        if (rc) return rc;
+        ch->post_open = false;
+        rc = server_wait(ch, ch->post_seq);
+        ch->ctx->dropin_ns[2] += now_ns() - ch->post_t0;
+        if (rc == kExitedEarly) return set_err(ch->ctx, TD_ERR_HIP, "chain server returned before answering twice");
     }
+    if (rc) return rc;
+    ch->ctx->dropin_ns[16] += 10 * *vol(&ch->mb_host->diag[1]);  // (100 MHz ticks)
+    ch->srv_pending = ch->post_steps[ch->post_nsteps - 1];
+    ch->srv_has_pending = ch->srv_pending.decision == kDecideLater;
     unpack_report(ch->script_host, ch->ctx->g.n, base_ptS, phi_out, ptS_out);
     return TD_OK;
 }
 
-int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val) {
+int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,
+                       double *phi_out, double *ptS_out) {
+    const int rc = shadow_server_post(ch, decision, steps, nsteps);
+    if (rc) return rc;
+    return shadow_server_answer(ch, base_ptS, phi_out, ptS_out);
+}
+
+// One-point query, split like the evaluate: post, then the answer (the caller classifies meanwhile).
+int shadow_server_query_post(td_chain *ch, double x, double y, double z, const ScriptStep *edit) {
+    if (ch->post_open) return set_err(ch->ctx, TD_ERR_ARG, "server: a command is open");
     int rc = server_start(ch);
     if (rc) return rc;
     if (g_post_delay_ms.load() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(g_post_delay_ms.load()));
@@ -1652,16 +1686,34 @@ int shadow_server_query(td_chain *ch, double x, double y, double z, const Script
     m->q[2] = z;
     m->has_edit = edit ? 1 : 0;
     if (edit) m->qedit = *edit;
-    const int64_t t0 = now_ns();
-    rc = server_post(ch);
-    ch->ctx->dropin_ns[5] += now_ns() - t0;
+    ch->post_held = edit ? *edit : ScriptStep{};
+    ch->post_had = edit != nullptr;
+    ch->post_t0 = now_ns();
+    ch->post_seq = m->seq + 1;
+    post_seq(m, ch->post_seq);
+    ch->post_open = true;
+    return TD_OK;
+}
+
+int shadow_server_query_answer(td_chain *ch, double *val) {
+    if (!ch->post_open) return set_err(ch->ctx, TD_ERR_ARG, "server: no query posted");
+    ch->post_open = false;
+    int rc = server_wait(ch, ch->post_seq);
+    ch->ctx->dropin_ns[5] += now_ns() - ch->post_t0;
     if (rc == TD_OK) ch->ctx->dropin_ns[17] += 10 * *vol(&ch->mb_host->diag[1]);
     // the kernel had returned (its pending proposal undone: the caller sees the server
     // stopped and re-issues that proposal's commit): answer with a one-off launch
-    if (rc == kExitedEarly) return shadow_chain_query(ch, x, y, z, edit, val);
+    const Mailbox *m = ch->mb_host;
+    if (rc == kExitedEarly) return shadow_chain_query(ch, m->q[0], m->q[1], m->q[2], ch->post_had ? &ch->post_held : nullptr, val);
     if (rc) return rc;
     *val = m->qval;
     return TD_OK;
+}
+
+int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val) {
+    const int rc = shadow_server_query_post(ch, x, y, z, edit);
+    if (rc) return rc;
+    return shadow_server_query_answer(ch, val);
 }
 
 int shadow_server_stop(td_chain *ch) { return server_stop(ch); }

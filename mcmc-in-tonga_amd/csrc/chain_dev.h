@@ -284,9 +284,14 @@ double shadow_chain_phi(const td_chain *ch);
 void shadow_chain_destroy(td_chain *ch);
 // server mode (a resident launch fed by a mailbox): decision = the pending proposal's fate
 bool shadow_server_alive(td_chain *ch);
+// the same split: post the command (no wait; one open at a time), then take its answer
+int shadow_server_post(td_chain *ch, int decision, const ScriptStep *steps, int nsteps);
+int shadow_server_answer(td_chain *ch, const double *base_ptS, double *phi_out, double *ptS_out);
 int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,
                        double *phi_out, double *ptS_out);
 int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val);
+int shadow_server_query_post(td_chain *ch, double x, double y, double z, const ScriptStep *edit);
+int shadow_server_query_answer(td_chain *ch, double *val);
 int shadow_server_stop(td_chain *ch);
 // Stop every resident server this thread runs except `keep` (nullable): called
 // before work on any other stream (chain.cpp t_servers).

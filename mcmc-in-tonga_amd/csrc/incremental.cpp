@@ -176,6 +176,116 @@ bool looks_like_q(const double *const in[4], int64_t M, const Cells &B, const Sc
     }
 }
 
+// Whether `in` (M cells) is an edit of Q = B + e rather than of B, from e's mark where any one further
+// edit leaves it (at its position, one lower after a death before it, or the whole count for a size
+// change) -- every one-edit sequence of TD_inversion_function.jl, O(1).  Where both readings give the
+// same model (a death of e's own cell, e's cell edited again) either base is right.
+bool descends_from_q(const double *const in[4], int64_t M, const Cells &B, const ScriptStep &e) {
+    const int64_t N = B.size(), k = e.index;
+    auto eq = [](double a, double b) { return std::memcmp(&a, &b, sizeof(double)) == 0; };
+    auto cell_is = [&](int64_t i, double x, double y, double zeta) {  // in[i] has this site and value
+        return i >= 0 && i < M && eq(in[0][i], x) && eq(in[1][i], y) && eq(in[3][i], zeta);
+    };
+    switch (e.action) {
+        case 1:  // birth: Q has N + 1 cells, e's at N
+            if (M == N + 2) return true;
+            if (M == N - 1) return false;
+            if (M == N + 1)  // Q changed / moved (its new cell keeps its site or its value), or B + a birth
+                return (eq(in[0][N], e.x) && eq(in[1][N], e.y)) || eq(in[3][N], e.zeta);
+            return M == N && cell_is(N - 1, e.x, e.y, e.zeta);  // Q less a cell before e's
+        case 2: {  // death of k: Q[i] = B[i + 1] from k on, N - 1 cells
+            if (M == N + 1) return false;
+            if (M == N - 2) return true;
+            const bool next_at_k = k + 1 < N && k < M && eq(in[0][k], B.x[(size_t)k + 1]) && eq(in[1][k], B.y[(size_t)k + 1]);
+            if (M == N) return next_at_k;  // Q + a birth (B + a change / move keeps B[k] at k)
+            // M == N - 1: Q changed / moved, or B less a cell (j < k puts B[k] at k - 1)
+            const bool below = k == 0 || (eq(in[0][k - 1], B.x[(size_t)k - 1]) && eq(in[3][k - 1], B.zeta[(size_t)k - 1]));
+            const bool at_k = k + 1 < N && k < M && (next_at_k || eq(in[3][k], B.zeta[(size_t)k + 1]));
+            return below && at_k;
+        }
+        case 3:  // change of k: e.zeta at k, or at k - 1 after a death before it
+            return (k < M && eq(in[3][k], e.zeta)) || (M == N - 1 && k >= 1 && eq(in[3][k - 1], e.zeta));
+        case 4:  // move of k: e's site at k, or at k - 1 after a death before it
+            return (k < M && eq(in[0][k], e.x) && eq(in[1][k], e.y)) ||
+                   (M == N - 1 && k >= 1 && eq(in[0][k - 1], e.x) && eq(in[1][k - 1], e.y));
+        default:
+            return false;
+    }
+}
+
+// The edit `in` (M cells) most likely makes to `v`, from its length and ONE field's first
+// difference (x, else zeta): what classify finds when `in` is v plus one reference-shaped edit.
+// Cheap (one array up to the edit), so the server can start on it while classify verifies.
+// false: no guess (v itself, or a shape the probe does not cover).
+bool probe_edit(const double *const in[4], int64_t M, const View &v, ScriptStep *e) {
+    const int64_t N = v.size();
+    std::memset(e, 0, sizeof *e);
+    auto first_diff = [&](int a, int64_t lim) -> int64_t {
+        int64_t k = 0;
+        while (k < lim) {
+            int64_t r;
+            const double *p = v.run(a, k, &r);
+            r = std::min(r, lim - k);
+            int64_t j = 0;
+            constexpr int64_t kBlk = 64;
+            while (j + kBlk <= r && bits_eq(in[a] + k + j, p + j, kBlk)) j += kBlk;
+            while (j < r && std::memcmp(in[a] + k + j, p + j, sizeof(double)) == 0) ++j;
+            k += j;
+            if (j < r) break;
+        }
+        return k;
+    };
+    auto at = [&](int a, int64_t j) {  // field a of v at position j
+        int64_t r;
+        return *v.run(a, j, &r);
+    };
+    auto same = [](double a, double b) { return std::memcmp(&a, &b, sizeof(double)) == 0; };
+    // O(1) spot checks of the guess (the last cell, the cells around the edit): they tell which of
+    // two bases a model descends from; classify proves it
+    if (M == N + 1) {  // birth: append! (:85-88)
+        if (!sane(in[0][N]) || !sane(in[1][N]) || !sane(in[2][N]) || !std::isfinite(in[3][N])) return false;
+        if (N > 0 && !(same(in[0][N - 1], at(0, N - 1)) && same(in[3][N - 1], at(3, N - 1)))) return false;
+        e->action = 1;
+        e->index = (int)N;
+        e->x = in[0][N];
+        e->y = in[1][N];
+        e->z = in[2][N];
+        e->zeta = in[3][N];
+        return true;
+    }
+    if (M == N - 1 && M >= 1) {  // death: deleteat! (:132-135) where x first differs
+        const int64_t p = first_diff(0, M);
+        if (!same(in[0][M - 1], at(0, N - 1)) || !same(in[3][M - 1], at(3, N - 1))) return false;
+        if (p < M && !(same(in[1][p], at(1, p + 1)) && same(in[3][p], at(3, p + 1)))) return false;
+        e->action = 2;
+        e->index = (int)p;
+        return true;
+    }
+    if (M == N && N >= 1) {
+        int64_t p = first_diff(0, N);
+        if (p < N) {  // move (:234-236)
+            if (!sane(in[0][p]) || !sane(in[1][p]) || !sane(in[2][p])) return false;
+            if (!same(in[3][p], at(3, p))) return false;  // (a move keeps the value)
+            if (p + 1 < N && !(same(in[0][N - 1], at(0, N - 1)) && same(in[3][N - 1], at(3, N - 1)))) return false;
+            e->action = 4;
+            e->index = (int)p;
+            e->x = in[0][p];
+            e->y = in[1][p];
+            e->z = in[2][p];
+            return true;
+        }
+        p = first_diff(3, N);
+        if (p < N && std::isfinite(in[3][p])) {  // change (:189)
+            if (p + 1 < N && !same(in[3][N - 1], at(3, N - 1))) return false;
+            e->action = 3;
+            e->index = (int)p;
+            e->zeta = in[3][p];
+            return true;
+        }
+    }
+    return false;
+}
+
 // Is `in` (M cells) the model `base` plus one reference-shaped edit?  0:
 // identical, 1: one edit (in *e, decision unset), -1: neither.
 int classify(const double *const in[4], int64_t M, const View &base, ScriptStep *e) {
@@ -325,6 +435,61 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
     // server mode (incremental == 2): one resident launch answers every call
     const bool srv = ctx->incremental == 2;
     if (s->dev_pending && !(srv && shadow_server_alive(s->ch))) s->dev_pending = false;  // stopped: undone
+    if (srv) {
+        // Optimistic: guess the base (Q where it holds Q's mark, else B) and the edit (probe_edit: one
+        // array scan), post that step to the server at once, and verify it with the full classify while
+        // the device evaluates.  The host state then is exactly what the checked path below would leave.
+        // A wrong guess (never, for a reference-shaped host) drops the shadow: the full evaluate answers.
+        const int64_t tp = now_ns();
+        const bool on_q = s->pending && descends_from_q(in, M, s->B, s->e);
+        ScriptStep g;
+        const bool guessed = probe_edit(in, M, on_q ? View(s->B, &s->e) : View(s->B, nullptr), &g);
+        if (guessed && (on_q || !s->pending || std::memcmp(&g, &s->e, sizeof g) != 0)) {
+            ScriptStep steps[kMaxScript];
+            int nsteps = 0, decision = 0;
+            if (on_q) {  // Julia went on from Q: the device commits it first
+                if (s->dev_pending) {
+                    decision = 1;
+                } else {
+                    ScriptStep c = posted(s->e, s->B);
+                    c.decision = 1;
+                    steps[nsteps++] = c;
+                }
+                s->B.apply(s->e);
+                s->phiB = s->phiQ;
+                s->ptSB.swap(s->ptSQ);
+            }
+            s->pending = false;  // (not on Q: Q, if any, was rejected -- undone, decision 0)
+            const int64_t after = s->B.size() + (g.action == 1 ? 1 : g.action == 2 ? -1 : 0);
+            if (after + 1 > shadow_chain_slots(s->ch) || after > 4 * std::max<int64_t>(s->built_n, 64)) {
+                s->last = s->B;  // rebuilt from B (a pending commit step is then moot)
+                s->last_phi = s->phiB;
+                s->last_ptS = s->ptSB;
+                s->have_last = true;
+                int rc = build_shadow(ctx, s);
+                if (rc) return rc;
+                nsteps = 0;
+            }
+            ctx->dropin_ns[1] += now_ns() - tp;
+            g.decision = kDecideLater;
+            steps[nsteps++] = posted(g, s->B);
+            g.decision = 0;
+            int rc = shadow_server_post(s->ch, decision, steps, nsteps);
+            ScriptStep v2;
+            const int rv = rc ? -1 : classify(in, M, View(s->B, nullptr), &v2);  // (the device works meanwhile)
+            s->ptSQ.assign((size_t)n, 0.0);
+            if (!rc) rc = shadow_server_answer(s->ch, s->ptSB.data(), &s->phiQ, s->ptSQ.data());
+            if (rc || rv != 1 || std::memcmp(&v2, &g, sizeof g) != 0) {
+                drop_chain(s);
+                s->have_last = false;
+                return rc ? rc : full();
+            }
+            s->e = g;
+            s->pending = true;
+            s->dev_pending = true;
+            return out(s->phiQ, s->ptSQ);
+        }
+    }
     // which state is the new model an edit of?
     const int64_t tc = now_ns();
     struct Lap {  // (the classification's time, however this call leaves)
@@ -415,6 +580,20 @@ int interpolate_incremental(td_ctx *ctx, const double *x, const double *y, const
     if (!s || !s->ch || !std::isfinite(qx) || !std::isfinite(qy) || !std::isfinite(qz)) return TD_OK;
     const double *in[4] = {x, y, z, zeta};
     ScriptStep e2;
+    if (s->dev_pending && !shadow_server_alive(s->ch)) s->dev_pending = false;
+    if (shadow_server_alive(s->ch)) {
+        // a running server: post the query on the model the cells most likely are (the pending proposal
+        // where they hold its mark, else the committed one) and verify that while it is answered
+        const bool on_q = s->pending && descends_from_q(in, M, s->B, s->e);
+        int rc = shadow_server_query_post(s->ch, qx, qy, qz, on_q ? &s->e : nullptr);
+        if (rc) return rc;
+        const int rb = classify(in, M, View(s->B, nullptr), &e2);  // (inside the round trip: not counted apart)
+        rc = shadow_server_query_answer(s->ch, val);
+        if (rc) return rc;
+        const bool ok = on_q ? (rb == 1 && s->pending && std::memcmp(&e2, &s->e, sizeof e2) == 0) : rb == 0;
+        *handled = ok ? 1 : 0;  // (a wrong guess: the plain path answers; nothing changed)
+        return TD_OK;
+    }
     const int64_t tc = now_ns();
     const int rb = classify(in, M, View(s->B, nullptr), &e2);
     ctx->dropin_ns[4] += now_ns() - tc;
