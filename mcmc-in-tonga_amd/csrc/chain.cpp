@@ -67,6 +67,7 @@ struct td_chain {
     bool post_had = false;
     long long post_seq = 0;
     int64_t post_t0 = 0;
+    long long pq_expect = -1;  // the death evaluate whose killed-site query the kernel answers ahead (pq_seq)
     td_rounds *rounds = nullptr;  // a resident tempering launch holds this chain (td_rounds_*)
 };
 
@@ -663,6 +664,8 @@ int server_start(td_chain *ch) {
     Mailbox *m = ch->mb_host;
     m->exited = 0;
     m->done = m->seq;
+    m->pq_seq = -1;
+    ch->pq_expect = -1;
     std::atomic_thread_fence(std::memory_order_release);
     hipError_t e = hipSuccess;
     if (ch->desc_dirty) {
@@ -1662,8 +1665,26 @@ int shadow_server_answer(td_chain *ch, const double *base_ptS, double *phi_out, 
     ch->ctx->dropin_ns[16] += 10 * *vol(&ch->mb_host->diag[1]);  // (100 MHz ticks)
     ch->srv_pending = ch->post_steps[ch->post_nsteps - 1];
     ch->srv_has_pending = ch->srv_pending.decision == kDecideLater;
+    ch->pq_expect = ch->srv_has_pending && ch->srv_pending.action == 2 ? ch->post_seq : -1;
     unpack_report(ch->script_host, ch->ctx->g.n, base_ptS, phi_out, ptS_out);
     return TD_OK;
+}
+
+// The pending death's Interpolation at its killed site (x, y, z), answered by the kernel right after the
+// evaluate (no command, no round trip): 1 and *val, or 0 (another point, nothing pending, no server).
+int shadow_server_death_query(td_chain *ch, double x, double y, double z, double *val) {
+    if (!ch->srv_running || ch->post_open || ch->pq_expect < 0 || !ch->srv_has_pending) return 0;
+    const ScriptStep &st = ch->srv_pending;
+    auto same = [](double a, double b) { return std::memcmp(&a, &b, sizeof(double)) == 0; };
+    if (st.action != 2 || !same(st.old[0], x) || !same(st.old[1], y) || !same(st.old[2], z)) return 0;
+    Mailbox *m = ch->mb_host;
+    const int64_t t0 = now_ns();
+    for (long long spin = 0; *vol(&m->pq_seq) != ch->pq_expect; ++spin)
+        if (*vol(&m->exited) || ((spin & 1023) == 1023 && now_ns() - t0 > 100000000)) return 0;  // (100 ms)
+    std::atomic_thread_fence(std::memory_order_acquire);
+    *val = *static_cast<volatile double *>(&m->pq_val);
+    ch->ctx->dropin_ns[5] += now_ns() - t0;
+    return 1;
 }
 
 int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,

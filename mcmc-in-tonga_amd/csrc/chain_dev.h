@@ -162,6 +162,10 @@ struct Mailbox {
     long long exited;  // the kernel has returned (its state is written back)
     double qval;
     long long diag[4];  // diagnostic: shader cycles and 100 MHz ticks of the last busy interval, polls
+    // a death evaluated with its fate pending: Interpolation of that proposed model at the killed site
+    // (TD_inversion_function.jl:146, the host's next call), stored after the answer; pq_seq = its command
+    double pq_val;
+    long long pq_seq;
 };
 
 // The command's words (seq first, check last) and their check: each payload word mixed with its
@@ -291,6 +295,7 @@ int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int 
                        double *phi_out, double *ptS_out);
 int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val);
 int shadow_server_query_post(td_chain *ch, double x, double y, double z, const ScriptStep *edit);
+int shadow_server_death_query(td_chain *ch, double x, double y, double z, double *val);
 int shadow_server_query_answer(td_chain *ch, double *val);
 int shadow_server_stop(td_chain *ch);
 // Stop every resident server this thread runs except `keep` (nullable): called

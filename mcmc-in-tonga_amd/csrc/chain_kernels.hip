@@ -466,13 +466,19 @@ __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf,
     const int ii = bi + nb % 3 - 1, jj = bj + (nb / 3) % 3 - 1, kk = bk + nb / 9 - 1;
     const bool inb = lane < 54 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
     const int b = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
-    const int cnt = d.bucket_count[b];
+    // global_ loads (vmcnt only): the scalar loads of the grid's fields below wait on lgkmcnt, which a
+    // flat_ load would hold until these loads are back
+    const int cnt = gload(d.bucket_count + b);
     CellEntry e[4];
     int sl[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        e[u] = d.buckets[b * kBucketCap + grp * 4 + u];
-        sl[u] = d.bslot[b * kBucketCap + grp * 4 + u];
+        const CellEntry *ep = d.buckets + b * kBucketCap + grp * 4 + u;
+        e[u].x = gload(&ep->x);
+        e[u].y = gload(&ep->y);
+        e[u].z = gload(&ep->z);
+        e[u].zeta = gload(&ep->zeta);
+        sl[u] = gload(d.bslot + b * kBucketCap + grp * 4 + u);
     }
     // every cell outside the 3x3x3 block is at least sqrt(lb) away: computed while the loads fly
     const double lb = grid_block_lb(G, x, y, z, 1);
@@ -2108,6 +2114,17 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     __builtin_amdgcn_s_waitcnt(0);
                     wave_sync_lds();
                     if (lane == 0) mb_store(&mb->done, sh.srv_seq);
+                    if (action == tdchain::kDeath) {
+                        // the reference next asks Interpolation of the proposed model at the killed site
+                        // (TD_inversion_function.jl:146): answered now, beside the host's own work, and
+                        // left in the mailbox under this command's seq (pq_val before pq_seq)
+                        const Nearest r = wave_nearest(d, v, sh, lane, kx, ky, kz, slot_k, -1, 0.0, 0.0, 0.0, 0.0);
+                        if (lane == 0) {
+                            mb_store(reinterpret_cast<long long *>(&mb->pq_val), __double_as_longlong(r.z));
+                            __builtin_amdgcn_s_waitcnt(0);
+                            mb_store(&mb->pq_seq, sh.srv_seq);
+                        }
+                    }
                     server_wait(mb, d, v, sh, lane);
                 }
                 __syncthreads();

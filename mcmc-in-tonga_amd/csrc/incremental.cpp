@@ -585,6 +585,16 @@ int interpolate_incremental(td_ctx *ctx, const double *x, const double *y, const
         // a running server: post the query on the model the cells most likely are (the pending proposal
         // where they hold its mark, else the committed one) and verify that while it is answered
         const bool on_q = s->pending && descends_from_q(in, M, s->B, s->e);
+        if (on_q && s->dev_pending && s->e.action == 2) {
+            // the death's query at its killed site (TD_inversion_function.jl:146): the kernel answered it
+            // right after the evaluate; the cells are checked meanwhile
+            const int rb = classify(in, M, View(s->B, nullptr), &e2);
+            if (rb == 1 && std::memcmp(&e2, &s->e, sizeof e2) == 0 &&
+                shadow_server_death_query(s->ch, qx, qy, qz, val)) {
+                *handled = 1;
+                return TD_OK;
+            }
+        }
         int rc = shadow_server_query_post(s->ch, qx, qy, qz, on_q ? &s->e : nullptr);
         if (rc) return rc;
         const int rb = classify(in, M, View(s->B, nullptr), &e2);  // (inside the round trip: not counted apart)
