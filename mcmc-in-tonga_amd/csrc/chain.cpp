@@ -1530,21 +1530,26 @@ double shadow_chain_phi(const td_chain *ch) { return ch->phi; }
 
 // The kernel's report [phi, k, (ray, ptS) x k] (k = -1: the whole ptS
 // follows) over the model's ptS `base` -> phi, the proposed model's ptS.
-void unpack_report(const double *buf, int64_t n, const double *base, double *phi, double *ptS) {
-    if (phi) *phi = buf[0];
-    if (!ptS || n == 0) return;
+int64_t unpack_report(const double *buf, int64_t n, const double *base, double *ptS) {
+    if (n == 0) return 0;
     const long long k = (long long)buf[1];
     if (k < 0) {
         std::memcpy(ptS, buf + 2, sizeof(double) * (size_t)n);
-        return;
+        return 0;
     }
     std::memcpy(ptS, base, sizeof(double) * (size_t)n);
-    for (long long i = 0; i < k; ++i) ptS[(size_t)buf[2 + 2 * i]] = buf[3 + 2 * i];
+    int64_t k0 = n;
+    for (long long i = 0; i < k; ++i) {
+        const int64_t r = (int64_t)buf[2 + 2 * i];
+        ptS[(size_t)r] = buf[3 + 2 * i];
+        k0 = std::min(k0, r);
+    }
+    return k0;
 }
 
 // Run 1..kMaxScript host-given steps in one k_chain_run launch; the step with
 // decision 0 (the last) leaves [phi_n, ptS_n] in the pinned output.
-int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, const double *base_ptS, double *phi_out,
+int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, const double *base_ptS, int64_t *k0_out,
                         double *ptS_out) {
     td_ctx *c = ch->ctx;
     if (nsteps < 1 || nsteps > kMaxScript) return set_err(c, TD_ERR_ARG, "shadow script");
@@ -1567,7 +1572,7 @@ int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, const
     if (e != hipSuccess) return hip_err(c, e, "k_chain_run (script)");
     adopt_scalars(ch);
     if (steps[nsteps - 1].decision == 0) {
-        unpack_report(ch->script_host, c->g.n, base_ptS, phi_out, ptS_out);
+        *k0_out = unpack_report(ch->script_host, c->g.n, base_ptS, ptS_out);
     }
     return TD_OK;
 }
@@ -1636,7 +1641,7 @@ int shadow_server_post(td_chain *ch, int decision, const ScriptStep *steps, int 
     return server_post_eval(ch, decision, steps, nsteps, false);
 }
 
-int shadow_server_answer(td_chain *ch, const double *base_ptS, double *phi_out, double *ptS_out) {
+int shadow_server_answer(td_chain *ch, const double *base_ptS, int64_t *k0_out, double *ptS_out) {
     if (!ch->post_open) return set_err(ch->ctx, TD_ERR_ARG, "server: no command posted");
     ch->post_open = false;
     int rc = server_wait(ch, ch->post_seq);
@@ -1666,7 +1671,7 @@ int shadow_server_answer(td_chain *ch, const double *base_ptS, double *phi_out, 
     ch->srv_pending = ch->post_steps[ch->post_nsteps - 1];
     ch->srv_has_pending = ch->srv_pending.decision == kDecideLater;
     ch->pq_expect = ch->srv_has_pending && ch->srv_pending.action == 2 ? ch->post_seq : -1;
-    unpack_report(ch->script_host, ch->ctx->g.n, base_ptS, phi_out, ptS_out);
+    *k0_out = unpack_report(ch->script_host, ch->ctx->g.n, base_ptS, ptS_out);
     return TD_OK;
 }
 
@@ -1688,10 +1693,10 @@ int shadow_server_death_query(td_chain *ch, double x, double y, double z, double
 }
 
 int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,
-                       double *phi_out, double *ptS_out) {
+                       int64_t *k0_out, double *ptS_out) {
     const int rc = shadow_server_post(ch, decision, steps, nsteps);
     if (rc) return rc;
-    return shadow_server_answer(ch, base_ptS, phi_out, ptS_out);
+    return shadow_server_answer(ch, base_ptS, k0_out, ptS_out);
 }
 
 // One-point query, split like the evaluate: post, then the answer (the caller classifies meanwhile).

@@ -279,8 +279,9 @@ hipError_t test_chain_chi2(const double *ptS, const double *tS, const double *si
 // draws -- it takes the caller's edits as scripted steps (ScriptStep).
 int shadow_chain_create(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                         int64_t ncells, int64_t cap, const double box[6], td_chain **out);
-// base_ptS: ptS of the model the last step edits (the report carries the changed rays only)
-int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, const double *base_ptS, double *phi_out,
+// base_ptS: ptS of the model the last step edits (the report carries the changed rays only);
+// *k0_out: the first ray whose t* changed (n: none) -- the caller forms phi_n (incremental.cpp)
+int shadow_chain_script(td_chain *ch, const ScriptStep *steps, int nsteps, const double *base_ptS, int64_t *k0_out,
                         double *ptS_out);
 int64_t shadow_chain_slots(const td_chain *ch);
 int64_t shadow_chain_ncells(const td_chain *ch);
@@ -290,9 +291,9 @@ void shadow_chain_destroy(td_chain *ch);
 bool shadow_server_alive(td_chain *ch);
 // the same split: post the command (no wait; one open at a time), then take its answer
 int shadow_server_post(td_chain *ch, int decision, const ScriptStep *steps, int nsteps);
-int shadow_server_answer(td_chain *ch, const double *base_ptS, double *phi_out, double *ptS_out);
+int shadow_server_answer(td_chain *ch, const double *base_ptS, int64_t *k0_out, double *ptS_out);
 int shadow_server_eval(td_chain *ch, int decision, const ScriptStep *steps, int nsteps, const double *base_ptS,
-                       double *phi_out, double *ptS_out);
+                       int64_t *k0_out, double *ptS_out);
 int shadow_server_query(td_chain *ch, double x, double y, double z, const ScriptStep *edit, double *val);
 int shadow_server_query_post(td_chain *ch, double x, double y, double z, const ScriptStep *edit);
 int shadow_server_death_query(td_chain *ch, double x, double y, double z, double *val);

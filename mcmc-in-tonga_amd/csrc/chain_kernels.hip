@@ -1004,6 +1004,29 @@ __device__ __attribute__((noinline)) double exact_sums(const double *term, doubl
     return phi;
 }
 
+// A scripted step's answer in the pinned output (wave 0; system-scope stores): [phi, k, (ray, ptS) x k],
+// the changed rays' new t* (the caller holds the model's ptS); k = -1: the whole proposed ptS follows.
+// phi: NaN when the answer goes out before phase F (a server's step: the host forms phi_n itself).
+__device__ void server_report(double *outp, const Views &v, const Shared &sh, int n, int lane, double phi) {
+    long long *out = reinterpret_cast<long long *>(outp);
+    auto put = [&](int i, double x) { mb_store(out + i, __double_as_longlong(x)); };
+    const int nr = sh.n_rays;
+    const bool few = 2 * nr + 2 <= n + 1;
+    if (few) {
+        for (int i = lane; i < nr; i += 64) {
+            const int r = v.ray_at(i);
+            put(2 + 2 * i, (double)r);
+            put(3 + 2 * i, v.cptS[r]);
+        }
+    } else {
+        for (int r = lane; r < n; r += 64) put(2 + r, v.rflag[r] ? v.cptS[r] : v.ptS[r]);
+    }
+    if (lane == 0) {
+        put(0, phi);
+        put(1, few ? (double)nr : -1.0);
+    }
+}
+
 // SCRIPT: host-given proposals (td_evaluate's incremental path: scripted
 // steps, the resident server); a free-running chain's instance has none of
 // that code on its path.
@@ -1331,8 +1354,11 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         double pre_bd = 0.0, pre_x = 0.0, pre_y = 0.0, pre_z = 0.0;
         if (p.active) {
             // ============ phase B: tile pass || birth/death Interpolation ============
-            // (a scripted step brings its own values: no Interpolation query)
-            const bool query = !nscript && (action == tdchain::kBirth || action == tdchain::kDeath);
+            // (a scripted step brings its own values: no Interpolation query -- but for a server's death
+            // step the reference next asks Interpolation of the proposed model at the killed site
+            // (TD_inversion_function.jl:146): the idle query wave answers it here, posted with the report)
+            const bool kill_q = SCRIPT && mb && action == tdchain::kDeath && sh.step_cur.decision == kDecideLater;
+            const bool query = (!nscript && (action == tdchain::kBirth || action == tdchain::kDeath)) || kill_q;
             if (eval) {
                 // tiles whose box can hold a point the proposal changes (the last
                 // wave answers the Interpolation query meanwhile)
@@ -1840,6 +1866,26 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 __syncthreads();
                 STAMP(4);
             }
+            // a server's step decided later: its answer goes out now, before phase F -- the changed rays'
+            // new t*, from which the host forms phi_n itself (the sequential sum from the first changed
+            // ray on its own partial sums, incremental.cpp), and a death's killed-site Interpolation
+            // (phase B); this step's exact sums below then overlap the host's work
+            const bool early = SCRIPT && mb && sh.step_cur.decision == kDecideLater;
+            if (early && wv == 0) {
+                server_report(sa.out, v, sh, n, lane, __builtin_nan(""));
+                // the answer's system-scope stores acknowledged before done: no system-scope
+                // fence, which would write back this XCD's L2 at every call
+                __builtin_amdgcn_s_waitcnt(0);
+                wave_sync_lds();
+                if (lane == 0) {
+                    mb_store(&mb->done, sh.srv_seq);
+                    if (action == tdchain::kDeath) {  // left in the mailbox under this command's seq
+                        mb_store(reinterpret_cast<long long *>(&mb->pq_val), __double_as_longlong(sh.q_zeta));
+                        __builtin_amdgcn_s_waitcnt(0);
+                        mb_store(&mb->pq_seq, sh.srv_seq);
+                    }
+                }
+            }
             // ==== phase F: chi^2 + decision (wave 0) || next proposal, tile maxima (rays in HBM) ====
             const long long tF = prof_on ? clock64() : 0;  // diagnostic: per-wave time in F
             constexpr bool spec_in_F = true;
@@ -2086,47 +2132,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             // ================= phase G: commit (or undo) =================
             const int nc = sh.n_changed, nr = sh.n_rays;
             const int sdec = nscript ? sh.step_cur.decision : 1;
-            if (nscript && sdec != 1 && wv == 0) {
-                // report phi_n and the changed rays' new ptS as [phi, k, (ray, ptS) x k] (the
-                // caller holds the model's ptS); k = -1: the whole proposed ptS follows
-                // (pinned host memory, written through system-scope stores: see below)
-                long long *out = reinterpret_cast<long long *>(sa.out);
-                auto put = [&](int i, double x) { mb_store(out + i, __double_as_longlong(x)); };
-                const bool few = 2 * nr + 2 <= n + 1;
-                if (few) {
-                    for (int i = lane; i < nr; i += 64) {
-                        const int r = v.ray_at(i);
-                        put(2 + 2 * i, (double)r);
-                        put(3 + 2 * i, v.cptS[r]);
-                    }
-                } else {
-                    for (int r = lane; r < n; r += 64) put(2 + r, v.rflag[r] ? v.cptS[r] : v.ptS[r]);
-                }
-                if (lane == 0) {
-                    put(0, sh.phi_n);
-                    put(1, few ? (double)nr : -1.0);
-                }
-            }
-            if (mb && sdec == kDecideLater) {  // answer the command, then its fate comes with the next one
-                if (wv == 0) {
-                    // the answer's system-scope stores acknowledged before done: no system-scope
-                    // fence, which would write back this XCD's L2 at every call
-                    __builtin_amdgcn_s_waitcnt(0);
-                    wave_sync_lds();
-                    if (lane == 0) mb_store(&mb->done, sh.srv_seq);
-                    if (action == tdchain::kDeath) {
-                        // the reference next asks Interpolation of the proposed model at the killed site
-                        // (TD_inversion_function.jl:146): answered now, beside the host's own work, and
-                        // left in the mailbox under this command's seq (pq_val before pq_seq)
-                        const Nearest r = wave_nearest(d, v, sh, lane, kx, ky, kz, slot_k, -1, 0.0, 0.0, 0.0, 0.0);
-                        if (lane == 0) {
-                            mb_store(reinterpret_cast<long long *>(&mb->pq_val), __double_as_longlong(r.z));
-                            __builtin_amdgcn_s_waitcnt(0);
-                            mb_store(&mb->pq_seq, sh.srv_seq);
-                        }
-                    }
-                    server_wait(mb, d, v, sh, lane);
-                }
+            if (nscript && sdec != 1 && !early && wv == 0) server_report(sa.out, v, sh, n, lane, sh.phi_n);
+            if (mb && sdec == kDecideLater) {  // answered before phase F; its fate comes with the next command
+                if (wv == 0) server_wait(mb, d, v, sh, lane);
                 __syncthreads();
                 if (tid == 0) acc_r = sh.accept != 0;
             }

@@ -57,11 +57,13 @@ struct td_shadow {
     Cells B;                 // committed model (Julia order), what the shadow chain holds
     double phiB = 0.0;
     std::vector<double> ptSB;
+    std::vector<double> preB;  // B's chi^2 partial sums (MCsub.jl:169-172): phi_n is formed here, from them
     bool pending = false;    // Q = B + e evaluated (undone on the device, or held there undecided: dev_pending)
     bool dev_pending = false;  // server mode: the resident kernel holds e's overlay, awaiting its fate
     ScriptStep e{};
     double phiQ = 0.0;
     std::vector<double> ptSQ;
+    std::vector<double> preQ;
     int64_t built_n = 0;     // cells when the shadow's bucket grid was sized
     // the last fully evaluated model, a shadow candidate
     bool have_last = false;
@@ -78,6 +80,26 @@ bool sane(double v) { return std::isfinite(v) && std::fabs(v) <= kSane; }
 
 bool bits_eq(const double *a, const double *b, int64_t n) {
     return n <= 0 || std::memcmp(a, b, sizeof(double) * (size_t)n) == 0;
+}
+
+// phi of ptS (MCsub.jl:169-172: C = 0, then C += ((ptS - tS)^2 * 1.0) / sig^2 in ray order), the
+// sequential sum resumed at ray k0 from the partial sums `pre` of a model whose t* agree with ptS below
+// k0 -- bit for bit the full sum (host_chi2), in O(n - k0).  `out` receives ptS's own partial sums.
+double chi2_resume(const td_ctx *ctx, const double *ptS, int64_t k0, const std::vector<double> &pre,
+                   std::vector<double> &out) {
+    const int64_t n = ctx->g.n;
+    const double *tS = ctx->tS_host.data(), *sig = ctx->sig_host.data();
+    out.resize((size_t)n);
+    k0 = std::max<int64_t>(0, std::min(k0, n));
+    if ((int64_t)pre.size() != n) k0 = 0;
+    double C = k0 > 0 ? pre[(size_t)k0 - 1] : 0.0;
+    if (k0 > 0 && &out != &pre) std::memcpy(out.data(), pre.data(), sizeof(double) * (size_t)k0);
+    for (int64_t k = k0; k < n; ++k) {
+        const double d = ptS[k] - tS[k];
+        C = C + ((d * d) * 1.0) / (sig[k] * sig[k]);
+        out[(size_t)k] = C;
+    }
+    return C;
 }
 
 // A model as the committed cells B plus at most one edit e (e.action 0: B
@@ -385,6 +407,7 @@ int build_shadow(td_ctx *ctx, td_shadow *s) {
     s->B = c;
     s->phiB = s->last_phi;
     s->ptSB = s->last_ptS;
+    chi2_resume(ctx, s->ptSB.data(), 0, s->preB, s->preB);  // (== phiB: the same sequential sum)
     s->pending = false;
     s->built_n = n;
     return TD_OK;
@@ -458,6 +481,7 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
                 s->B.apply(s->e);
                 s->phiB = s->phiQ;
                 s->ptSB.swap(s->ptSQ);
+                s->preB.swap(s->preQ);
             }
             s->pending = false;  // (not on Q: Q, if any, was rejected -- undone, decision 0)
             const int64_t after = s->B.size() + (g.action == 1 ? 1 : g.action == 2 ? -1 : 0);
@@ -477,8 +501,10 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
             int rc = shadow_server_post(s->ch, decision, steps, nsteps);
             ScriptStep v2;
             const int rv = rc ? -1 : classify(in, M, View(s->B, nullptr), &v2);  // (the device works meanwhile)
-            s->ptSQ.assign((size_t)n, 0.0);
-            if (!rc) rc = shadow_server_answer(s->ch, s->ptSB.data(), &s->phiQ, s->ptSQ.data());
+            s->ptSQ.resize((size_t)n);
+            int64_t k0 = 0;
+            if (!rc) rc = shadow_server_answer(s->ch, s->ptSB.data(), &k0, s->ptSQ.data());
+            if (!rc) s->phiQ = chi2_resume(ctx, s->ptSQ.data(), k0, s->preB, s->preQ);
             if (rc || rv != 1 || std::memcmp(&v2, &g, sizeof g) != 0) {
                 drop_chain(s);
                 s->have_last = false;
@@ -534,6 +560,7 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
         s->B.apply(s->e);  // B := Q (in place: O(1) but for a death's shift)
         s->phiB = s->phiQ;
         s->ptSB.swap(s->ptSQ);
+        s->preB.swap(s->preQ);
         s->pending = false;
     } else {
         return full();
@@ -553,9 +580,11 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
     lap.stop();
     e2.decision = srv ? kDecideLater : 0;
     steps[nsteps++] = posted(e2, s->B);
-    s->ptSQ.assign((size_t)n, 0.0);
-    int rc = srv ? shadow_server_eval(s->ch, decision, steps, nsteps, s->ptSB.data(), &s->phiQ, s->ptSQ.data())
-                 : shadow_chain_script(s->ch, steps, nsteps, s->ptSB.data(), &s->phiQ, s->ptSQ.data());
+    s->ptSQ.resize((size_t)n);
+    int64_t k0 = 0;
+    int rc = srv ? shadow_server_eval(s->ch, decision, steps, nsteps, s->ptSB.data(), &k0, s->ptSQ.data())
+                 : shadow_chain_script(s->ch, steps, nsteps, s->ptSB.data(), &k0, s->ptSQ.data());
+    if (!rc) s->phiQ = chi2_resume(ctx, s->ptSQ.data(), k0, s->preB, s->preQ);
     if (rc) {
         drop_chain(s);
         s->have_last = false;
