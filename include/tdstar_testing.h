@@ -42,6 +42,10 @@ int tdt_chain_profile(td_chain *ch, int enable, int64_t out[80]);
  * order mirrored), [1] bytes of the HBM layout, [2] 1 if the HBM layout holds
  * its super-tiles in LDS, [3] 1 if runs take the LDS layout. */
 int tdt_chain_lds(td_chain *ch, int64_t out[4]);
+/* Cycles of nq back-to-back nearest-cell queries through the chain's bucket grid by one wave
+ * (pts: nq x {x, y, z}); mode 0: the whole query, 1: its loads only, 2: its arithmetic only.
+ * out[0] = cycles, out[1] = unproven queries (full scans). */
+int tdt_chain_query_lat(td_chain *ch, const double *pts, int nq, int mode, int64_t out[4]);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);

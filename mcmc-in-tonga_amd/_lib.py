@@ -94,6 +94,7 @@ SIGNATURES = {
     "tdt_propose": (ctypes.c_int, [ctypes.POINTER(TdChainParams), _u64, _i64, _pd, _pd, _pd, _pd, _d, _pd]),
     "tdt_chain_profile": (ctypes.c_int, [_vp, ctypes.c_int, _pi64]),
     "tdt_chain_lds": (ctypes.c_int, [_vp, _pi64]),
+    "tdt_chain_query_lat": (ctypes.c_int, [_vp, _pd, ctypes.c_int, ctypes.c_int, _pi64]),
     "tdt_set_nn_method": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_nn_bench": (ctypes.c_int, [_vp, _pd, _pd, _pd, _pd, _i64, ctypes.c_int, ctypes.c_int, _pd]),
     "tdt_chain_set_lds_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
@@ -130,7 +131,10 @@ def lib():
             raise ImportError("libtdstar.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                               "(hipcc --offload-arch=gfx950); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
+        older = "TD_LIB_PATH" in os.environ  # (an A/B against an older build: newer testing hooks may be absent)
         for name, (res, args) in SIGNATURES.items():
+            if older and name.startswith("tdt_") and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -1833,6 +1833,29 @@ int tdt_chain_lds(td_chain *ch, int64_t out[4]) {
     return TD_OK;
 }
 
+int tdt_chain_query_lat(td_chain *ch, const double *pts, int nq, int mode, int64_t out[4]) {
+    if (!ch || ch->engine != TD_ENGINE_DEVICE || !pts || nq < 1 || !out) return TD_ERR_ARG;
+    td_ctx *c = ch->ctx;
+    double *dp = nullptr;
+    long long *dout = nullptr;
+    hipError_t e = hipMalloc((void **)&dp, sizeof(double) * 3 * (size_t)nq);
+    if (e == hipSuccess) e = hipMalloc((void **)&dout, sizeof(long long) * 4);
+    if (e == hipSuccess) e = hipMemcpy(dp, pts, sizeof(double) * 3 * (size_t)nq, hipMemcpyHostToDevice);
+    if (e == hipSuccess && ch->desc_dirty) {
+        e = hipMemcpy(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice);
+        ch->desc_dirty = false;
+    }
+    if (e == hipSuccess) e = test_query_lat(ch->dev_ptr, dp, nq, mode, dout, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    long long h[4] = {0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpy(h, dout, sizeof h, hipMemcpyDeviceToHost);
+    if (dp) (void)hipFree(dp);
+    if (dout) (void)hipFree(dout);
+    if (e != hipSuccess) return hip_err(c, e, "tdt_chain_query_lat");
+    for (int k = 0; k < 4; ++k) out[k] = h[k];
+    return TD_OK;
+}
+
 int tdt_chain_profile(td_chain *ch, int enable, int64_t out[80]) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE) return TD_ERR_ARG;
     ch->dev.profile = enable;

@@ -196,7 +196,50 @@ __device__ __forceinline__ void script_proposal(PState &o, const ScriptStep &st,
     o.eval = 1;
 }
 
+// The bucket grid's geometry and arrays, copied into LDS when a launch starts: a query reads them in
+// one round of LDS loads rather than one scalar load (and wait) per descriptor field, and bounds the
+// block without branches (wave_grid_search)
+struct GridGeo {
+    double x0, y0, z0, ix, iy, iz, hx, hy, hz, ex, ey, ez;
+    double lo[3], hi[3];
+    // a bound every query may use first: each face of a query's 3x3x3 block is at least h - e (the
+    // cells' allowance) - e (the query's own bucket rounding, within the same allowance) away on its
+    // axis, so every cell outside the block is at least lb0 away (+inf when no axis can have a face)
+    double lb0;
+    const int *count;
+    const CellEntry *buckets;
+    const int *bslot;
+    int gx, gy, gz, sealed;
+};
+__device__ __forceinline__ void geo_fill(GridGeo &g, const DevChain &d) {
+    const CellGrid &G = d.grid;
+    g.x0 = G.x0; g.y0 = G.y0; g.z0 = G.z0;
+    g.ix = G.ix; g.iy = G.iy; g.iz = G.iz;
+    g.hx = G.hx; g.hy = G.hy; g.hz = G.hz;
+    g.ex = G.ex; g.ey = G.ey; g.ez = G.ez;
+    for (int a = 0; a < 3; ++a) {
+        g.lo[a] = G.lo[a];
+        g.hi[a] = G.hi[a];
+    }
+    g.count = d.bucket_count;
+    g.buckets = d.buckets;
+    g.bslot = d.bslot;
+    g.gx = G.gx; g.gy = G.gy; g.gz = G.gz;
+    g.sealed = G.sealed;
+    const double h3[3] = {G.hx, G.hy, G.hz}, e3[3] = {G.ex, G.ey, G.ez};
+    const int g3[3] = {G.gx, G.gy, G.gz};
+    double lb0 = __builtin_huge_val();
+    for (int a = 0; a < 3; ++a) {
+        if (g3[a] < 3) continue;  // the block spans the axis: no face on it
+        const double gap = (h3[a] - 2.0 * e3[a]) * (1.0 - 0x1p-30);
+        const double f = gap > 0.0 ? gap * gap : 0.0;
+        lb0 = f < lb0 ? f : lb0;
+    }
+    g.lb0 = grid_lb_close(lb0);
+}
+
 struct Shared {
+    GridGeo geo;       // the bucket grid (geo_fill at a launch's start)
     PState ps[2];      // this iteration's proposal (ps[cur]) and the next one guessed in phase F
     int cur, spec_ok;
     int defer;  // phase F: accepted on bounds (LDS layout): the new chi^2 partial sums are not formed
@@ -528,11 +571,107 @@ __device__ __forceinline__ Nearest wave_grid_search(const DevChain &d, bool ovf,
     return res;
 }
 
+// wave_grid_search on the LDS copy of the grid: the same loads, the same answer and the same proof
+// (grid_block_lb's bound, R = 1, each face taken by a select instead of a branch)
+__device__ __forceinline__ Nearest wave_grid_search(const GridGeo &gl, bool ovf, int lane, double x, double y,
+                                                    double z, int skip, int moved, double mx, double my, double mz,
+                                                    double mzeta) {
+    const GridGeo G = gl;  // (one round of LDS loads, every lane the same words)
+    const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
+              bk = grid_axis(z, G.z0, G.iz, G.gz);
+    const int nb = lane % 27, grp = lane / 27;
+    const int ii = bi + nb % 3 - 1, jj = bj + (nb / 3) % 3 - 1, kk = bk + nb / 9 - 1;
+    const bool inb = lane < 54 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
+    const int b = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
+    const int cnt = gload(G.count + b);
+    CellEntry e[4];
+    int sl[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const CellEntry *ep = G.buckets + b * kBucketCap + grp * 4 + u;
+        e[u].x = gload(&ep->x);
+        e[u].y = gload(&ep->y);
+        e[u].z = gload(&ep->z);
+        e[u].zeta = gload(&ep->zeta);
+        sl[u] = gload(G.bslot + b * kBucketCap + grp * 4 + u);
+    }
+    double bd = kSentinel, bz = 0.0;
+    int bs = -1;
+    bool tie = false;
+    const bool overfull = inb && cnt > 8;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const bool ok = inb && grp * 4 + u < cnt && sl[u] != skip && sl[u] != moved;
+        const double dd = dist2(e[u].x, e[u].y, e[u].z, x, y, z);
+        if (ok) {
+            if (dd < bd) {
+                bd = dd;
+                bs = sl[u];
+                bz = e[u].zeta;
+                tie = false;
+            } else if (dd == bd && dd < kSentinel) {
+                tie = true;
+            }
+        }
+    }
+    if (lane == 63 && moved >= 0) {  // the moved cell, at its proposed site
+        const double dd = dist2(mx, my, mz, x, y, z);
+        if (dd < bd) {
+            bd = dd;
+            bs = moved;
+            bz = mzeta;
+            tie = false;
+        } else if (dd == bd && dd < kSentinel) {
+            tie = true;
+        }
+    }
+    const unsigned long long key = (unsigned long long)__double_as_longlong(bd);
+    const unsigned long long kmin = wave_min_u64_2p(key);
+    const unsigned long long who = __ballot(key == kmin);
+    const int win = __builtin_ctzll(who);
+    Nearest res;
+    res.d = __longlong_as_double((long long)kmin);
+    const bool found = res.d < kSentinel;
+    const bool tied = found && (__popcll(who) > 1 || __builtin_amdgcn_readlane((int)tie, win) != 0);
+    const bool any_over = __ballot(overfull) != 0ull;
+    res.s = found ? __builtin_amdgcn_readlane(bs, win) : -1;
+    res.z = found ? readlane_f64(bz, win) : 0.0;
+    res.proven = !ovf && !tied && !any_over && res.d < G.lb0;
+    if (!res.proven && !ovf && !tied && !any_over) {  // (wave-uniform; rare) the query's own block bound
+        double lb;
+        {
+            const double v[3] = {x, y, z}, e3[3] = {G.ex, G.ey, G.ez};
+            double o2[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {  // grid_out2
+                const double below = G.lo[a] - v[a], above = v[a] - G.hi[a];
+                const double o = (below > above ? below : above) - e3[a];
+                o2[a] = (G.sealed && o > 0.0) ? o * o : 0.0;
+            }
+            lb = __builtin_huge_val();
+            auto face = [&lb](double w, double w0, double h, double e1, int g, int i, double other) {
+                const double gl0 = (w - (w0 + (double)(i - 1) * h)) - e1;
+                const double gh0 = ((w0 + (double)(i + 2) * h) - w) - e1;
+                const double fl = (gl0 > 0.0 ? gl0 * gl0 : 0.0) + other;
+                const double fh = (gh0 > 0.0 ? gh0 * gh0 : 0.0) + other;
+                lb = (i - 1 > 0 && fl < lb) ? fl : lb;
+                lb = (i + 1 < g - 1 && fh < lb) ? fh : lb;
+            };
+            face(x, G.x0, G.hx, G.ex, G.gx, bi, o2[1] + o2[2]);
+            face(y, G.y0, G.hy, G.ey, G.gy, bj, o2[0] + o2[2]);
+            face(z, G.z0, G.hz, G.ez, G.gz, bk, o2[0] + o2[1]);
+            lb = grid_lb_close(lb);
+        }
+        res.proven = res.d < lb;
+    }
+    return res;
+}
+
 // Nearest live cell for one query, one wave: grid first, full scan if unproven.
 __device__ __forceinline__ Nearest wave_nearest(const DevChain &d, const Views &v, Shared &sh, int lane, double x,
                                                 double y, double z, int skip, int moved, double mx, double my,
                                                 double mz, double mzeta) {
-    Nearest r = wave_grid_search(d, sh.grid_ovf != 0, lane, x, y, z, skip, moved, mx, my, mz, mzeta);
+    Nearest r = wave_grid_search(sh.geo, sh.grid_ovf != 0, lane, x, y, z, skip, moved, mx, my, mz, mzeta);
     if (!r.proven) {
         if (lane == 0) atomicAdd(&sh.grid_fallbacks32, 1);
         r = wave_full_scan(d.stamp, d.cx, d.cy, d.cz, d.czeta, d.cap, sh.nslots, lane, x, y, z, skip, moved,
@@ -1167,6 +1306,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         sh.defer = 0;
         if (!RLDS) sh.dsum = sh.dabs = 0.0;
         sh.grid_fallbacks32 = 0;
+        geo_fill(sh.geo, d);
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
         sh.ncells = s0.ncells;
@@ -2439,6 +2579,7 @@ __global__ __launch_bounds__(64) void k_chain_query(const DevChain *__restrict__
         sh.grid_ovf = *d.grid_overflow;
         sh.nslots = d.st->nslots;
         sh.grid_fallbacks32 = 0;
+        geo_fill(sh.geo, d);
     }
     __syncthreads();
     Views v{};
@@ -2565,6 +2706,93 @@ hipError_t chain_full_state(DevChain &d, int ncells, NNWork &work, int num_cus, 
         e = hipGetLastError();
     }
     return e;
+}
+
+// Testing: the latency of a nearest-cell query through the chain's bucket grid, as phases B and D run
+// it: one wave answers nq queries back to back, each point offset by 0 * the previous answer (no two
+// overlap).  mode 0: wave_nearest; 1: its loads only (the sum of what they bring); 2: its arithmetic only
+// (the loads replaced by values made from the lane).  out[0] = cycles, out[1] = unproven queries.
+__global__ __launch_bounds__(64) void k_test_query_lat(const DevChain *__restrict__ dptr, const double *__restrict__ pts,
+                                                        int nq, int mode, long long *out) {
+    __shared__ Shared sh;
+    const DevChain &d = *dptr;
+    const int lane = threadIdx.x;
+    Views v{};
+    v.ord = d.order;
+    if (lane == 0) {
+        sh.grid_ovf = *d.grid_overflow;
+        sh.grid_fallbacks32 = 0;
+        sh.nslots = d.st->nslots;
+        geo_fill(sh.geo, d);
+    }
+    __syncthreads();
+    double acc = 0.0;
+    unsigned long long hsh = 0xcbf29ce484222325ull;
+    const long long t0 = clock64();
+    for (int i = 0; i < nq; ++i) {
+        const double k = acc * 0.0;
+        const double x = pts[3 * i] + k, y = pts[3 * i + 1] + k, z = pts[3 * i + 2] + k;
+        if (mode == 0 || mode == 6) {  // 6: the descriptor-reading search (d.grid), for comparison
+            const Nearest r = mode == 0 ? wave_grid_search(sh.geo, sh.grid_ovf != 0, lane, x, y, z, -1, -1, 0.0, 0.0,
+                                                           0.0, 0.0)
+                                        : wave_grid_search(d, sh.grid_ovf != 0, lane, x, y, z, -1, -1, 0.0, 0.0,
+                                                           0.0, 0.0);
+            acc = r.z;
+            // (a digest of every answer: the two searches must agree)
+            hsh = hsh * 0x100000001b3ull ^ (unsigned long long)__double_as_longlong(r.d) ^
+                  ((unsigned long long)(unsigned)r.s << 1) ^ (unsigned long long)r.proven;
+        } else {
+            const CellGrid &G = d.grid;
+            const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
+                      bk = grid_axis(z, G.z0, G.iz, G.gz);
+            const int nb = lane % 27, grp = lane / 27;
+            const int ii = bi + nb % 3 - 1, jj = bj + (nb / 3) % 3 - 1, kk = bk + nb / 9 - 1;
+            const bool inb = lane < 54 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
+            const int b = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
+            double t = 0.0;
+            if (mode == 3) {  // the bucket indices alone
+                t = (double)(b + grp);
+            } else if (mode == 4) {  // the block's face bound alone
+                t = grid_block_lb(G, x, y, z, 1);
+            } else if (mode == 5) {  // one lexicographic wave minimum alone
+                t = (double)wave_min_u64((unsigned long long)(b + lane));
+            } else if (mode == 1) {
+                const int cnt = gload(d.bucket_count + b);
+                double a = 0.0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const CellEntry *ep = d.buckets + b * kBucketCap + grp * 4 + u;
+                    a = a + gload(&ep->x) + gload(&ep->y) + gload(&ep->z) + gload(&ep->zeta) +
+                        (double)gload(d.bslot + b * kBucketCap + grp * 4 + u);
+                }
+                t = a + (double)cnt;
+                t = wave_sum_f64(t);
+            } else {
+                double bd = kSentinel;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double dd = dist2((double)b, (double)u, (double)lane, x, y, z);
+                    bd = dd < bd ? dd : bd;
+                }
+                const double lb = grid_block_lb(G, x, y, z, 1);
+                const unsigned long long kmin = wave_min_u64((unsigned long long)__double_as_longlong(bd));
+                t = __longlong_as_double((long long)kmin) < lb ? 1.0 : 2.0;
+            }
+            acc = t;
+        }
+    }
+    const long long t1 = clock64();
+    if (lane == 0) {
+        out[0] = t1 - t0;
+        out[1] = sh.grid_fallbacks32;
+        out[2] = __double_as_longlong(acc);
+        out[3] = (long long)hsh;
+    }
+}
+
+hipError_t test_query_lat(const DevChain *dev, const double *pts, int nq, int mode, long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_test_query_lat, dim3(1), dim3(64), 0, s, dev, pts, nq, mode, out);
+    return hipGetLastError();
 }
 
 hipError_t chain_query(const DevChain *dev, double x, double y, double z, const ScriptStep *edit, double *out,

@@ -56,6 +56,28 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
     return ((unsigned long long)hi << 32) | lo;
 }
+// min over the 64 lanes of 32-bit unsigned values, returned to every lane (one DPP min per step)
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+    constexpr int I = -1;  // ~0u
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(I, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+// wave_min_u64 as two 32-bit passes: the high words' minimum, then (only if several lanes hold it)
+// the low words' among those lanes -- the same 64-bit minimum, in a third of the dependent VALU steps
+__device__ __forceinline__ unsigned long long wave_min_u64_2p(unsigned long long v) {
+    const unsigned hi = (unsigned)(v >> 32), lo = (unsigned)v;
+    const unsigned mh = wave_min_u32(hi);
+    const unsigned long long at = __ballot(hi == mh);
+    unsigned ml;
+    if (__popcll(at) == 1) ml = (unsigned)__builtin_amdgcn_readlane((int)lo, __builtin_ctzll(at));  // (wave-uniform)
+    else ml = wave_min_u32(hi == mh ? lo : ~0u);
+    return ((unsigned long long)mh << 32) | ml;
+}
 // max over each row of 16 lanes, valid in the row's last lane (lane % 16 == 15)
 __device__ __forceinline__ unsigned long long row_max_u64(unsigned long long v) {
     v = umax64(v, dpp_u64<0x111, 0xf>(v, 0ull));
