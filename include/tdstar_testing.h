@@ -49,6 +49,12 @@ int tdt_chain_query_lat(td_chain *ch, const double *pts, int nq, int mode, int64
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);
+/* The device chain's decision pre-filter on a bracket of (phi, phi_n) (chain_logic.h decide_sure):
+ * 1 = accepted at every point of [phi_lo, phi_hi] x [phin_lo, phin_hi], -1 = rejected at every point,
+ * 0 = undecided (the kernel then evaluates the corners with the acceptance rule itself). */
+int tdt_decide_sure(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells,
+                    double phi_lo, double phi_hi, double phin_lo, double phin_hi, double czeta, double zeta_killed,
+                    double zetanew_death);
 /* Device engine layout: 0 (default) mirrors tiles, rays and the Julia order
  * in LDS when they fit (the 381-ray configs); 1 keeps them in HBM, the path
  * larger geometries take; 2 runs the 4-wave kernel that puts two chains on a

@@ -112,6 +112,8 @@ SIGNATURES = {
     "tdt_shadow_profile": (ctypes.c_int, [_vp, _pi64]),
     "tdt_chi2": (ctypes.c_int, [_vp, _pd, ctypes.c_int, _pd]),
     "tdt_accept": (ctypes.c_int, [ctypes.POINTER(TdChainParams), ctypes.c_int, _d, _d, _i64, _d, _d, _d, _d, _d]),
+    "tdt_decide_sure": (ctypes.c_int, [ctypes.POINTER(TdChainParams), ctypes.c_int, _d, _d, _i64, _d, _d, _d, _d, _d,
+                                       _d, _d]),
 }
 
 _lib = None

@@ -1884,5 +1884,25 @@ int tdt_accept(const td_chain_params *prm, int action, double u_accept, double z
     return tdchain::accept(P, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN) ? 1 : 0;
 }
 
+// The device's decision pre-filter (chain_logic.h decide_sure) on the bracket [phi_lo, phi_hi] x
+// [phin_lo, phin_hi]: 1 (accept everywhere), -1 (reject everywhere) or 0 (undecided).
+int tdt_decide_sure(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells,
+                    double phi_lo, double phi_hi, double phin_lo, double phin_hi, double czeta, double zeta_killed,
+                    double zetanew_death) {
+    const tdchain::Params P = make_params(*prm);
+    tdchain::Proposal p{};
+    p.action = action;
+    p.active = 1;
+    p.valid = 1;
+    p.u_accept = u_accept;
+    p.zeta = zeta_new;
+    if (action == tdchain::kBirth || action == tdchain::kChange) p.valid = tdchain::prior_valid(P, zeta_new);
+    p.log_u = u_accept > 0.0 ? tdchain::det_log(u_accept) : -HUGE_VAL;
+    double lnN[3];
+    tdchain::log_window(lnN, ncells);
+    const tdchain::AlphaParts a = tdchain::alpha_parts(P, p, czeta, zeta_killed, zetanew_death, lnN);
+    return tdchain::decide_sure(a, p.log_u, (phi_lo - phin_hi) * P.inv_2t, (phi_hi - phin_lo) * P.inv_2t);
+}
+
 
 }  // extern "C"

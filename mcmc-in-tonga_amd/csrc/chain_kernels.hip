@@ -65,6 +65,15 @@ constexpr int kBatchBuckets = 512;  // buckets in the region at most  // rays in
 // costs ~1.2k more cycles per proposal at 381 rays x 5000 cells)
 constexpr bool kSmallWalk = false;
 
+// A changed point's candidate (what mark() stores in the overlay), kept in LDS for the first kChgLds of
+// a proposal: phase G commits them from here with stores only -- no dependent round trips to the
+// changed list and the overlay in HBM
+struct ChgRec {
+    int q, s;
+    double d, z;
+};
+constexpr int kChgLds = 64;
+
 // A point whose nearest cell is removed or moved: re-searched in phase D.
 struct OrphanRec {
     double x, y, z;
@@ -283,6 +292,8 @@ struct Shared {
     long long srv_seq, srv_busy_c, srv_busy_w;
     long long mbox[40];  // server mode: the last command read from the mailbox
     OrphanRec orph[kOrphanLds];
+    ChgRec chg[kChgLds];
+    tdchain::AlphaParts ap;  // the decision's phi-free part (phase C, last wave), for phase F
     DeltaSegs dseg;  // rays in HBM: phase F's new chi^2 partial sums as segments over the old ones
     long long prof[kProfSlots], t_last, t_iter;  // diagnostic phase stamps
     // rays in HBM: the committed terms' sum kept in any order, |tsum - (the exact real sum)| <=
@@ -759,7 +770,9 @@ __device__ __forceinline__ void mark(const DevChain &d, const Views &v, Shared &
     d.cand_d[p] = dd;
     d.cand_z[p] = z;
     d.cand_flag[p] = 1;
-    d.changed[atomicAdd(&sh.n_changed, 1)] = p;
+    const int c = atomicAdd(&sh.n_changed, 1);
+    d.changed[c] = p;
+    if (c < kChgLds) sh.chg[c] = ChgRec{p, s, dd, z};
     if (atomicExch(&v.rflag[r], 1) == 0) {
         v.ray_put(atomicAdd(&sh.n_rays, 1), r);
         atomicMin(&sh.k0, r);
@@ -1660,6 +1673,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             int no = 0;
             if (fwd) {
                 // ================= phase C: affected points =================
+                if (!nscript && tid == NTH - 64)  // the decision's phi-free part, off phase F's path
+                    sh.ap = tdchain::alpha_parts(P, pp, czeta, zeta_killed, zetanew_death, sh.lnN);
 
                 const int nt = sh.n_tiles;
                 // the selected cell's value, known since the proposal was made: czeta[slot_k] = zeta_killed
@@ -2114,7 +2129,13 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                             // the sequential phi_n lies within (n - 1) ulps of the exact sum, far inside 1e-9
                             const double b_lo = (Sa - Ea) * (1.0 - 1e-9), b_hi = (Sa + Ea) * (1.0 + 1e-9);
-                            {  // the two corners side by side: lane 0 (phi_lo, b_hi), lane 1 (phi_hi, b_lo)
+                            // most decisions at once from the phi-free part (chain_logic.h decide_sure),
+                            // else the two corners side by side: lane 0 (phi_lo, b_hi), lane 1 (phi_hi, b_lo)
+                            const int sure = tdchain::decide_sure(sh.ap, pp.log_u, (sh.phi_lo - b_hi) * inv2t_r,
+                                                                  (sh.phi_hi - b_lo) * inv2t_r);
+                            if (sure != 0) {
+                                bdec = sure > 0 ? 2 : 1;
+                            } else {
                                 const bool lo = lane == 0;
                                 const int a = lane < 2 ? (int)tdchain::accept_t(P, inv2t_r, pp, lo ? sh.phi_lo : sh.phi_hi,
                                                                                lo ? b_hi : b_lo, czeta, zeta_killed,
@@ -2287,11 +2308,19 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 const int nt = sh.n_tiles, k0 = sh.k0;
                 if (wv != 0)
                     for (int c = w; c < nc; c += kW) {
-                        const int q = d.changed[c];
-                        d.best_s[q] = d.cand_s[q];
-                        d.best_d[q] = d.cand_d[q];
-                        d.zeta0[q] = d.cand_z[q];
-                        d.cand_flag[q] = 0;
+                        if (c < kChgLds) {  // (LDS: stores only)
+                            const ChgRec r = sh.chg[c];
+                            d.best_s[r.q] = r.s;
+                            d.best_d[r.q] = r.d;
+                            d.zeta0[r.q] = r.z;
+                            d.cand_flag[r.q] = 0;
+                        } else {
+                            const int q = d.changed[c];
+                            d.best_s[q] = d.cand_s[q];
+                            d.best_d[q] = d.cand_d[q];
+                            d.zeta0[q] = d.cand_z[q];
+                            d.cand_flag[q] = 0;
+                        }
                     }
                 if (fwd && action != tdchain::kChange) {
                     for (int i = tid; i < nt; i += NTH) v.tmaxd[v.tile_rec(i).x] = v.ctm_at(i);
@@ -2415,7 +2444,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 }
             } else {  // rejected: flags down, the changed rays get their old chi^2 terms back
                 if (wv != 0)
-                    for (int c = w; c < nc; c += kW) d.cand_flag[d.changed[c]] = 0;
+                    for (int c = w; c < nc; c += kW) d.cand_flag[c < kChgLds ? sh.chg[c].q : d.changed[c]] = 0;
                 for (int rr = tid; rr < nr; rr += NTH) {
                     const int r = v.ray_at(rr);
                     v.term[r] = v.cterm[r];

@@ -384,6 +384,52 @@ TD_HD bool accept(const Params &P, const Proposal &p, double phi, double phi_n, 
     return accept_t(P, P.inv_2t, p, phi, phi_n, czeta, zeta_killed, zetanew_death, lnN);
 }
 
+// The decision's phi-free part, for deciding a bracket of (phi, phi_n) with one add and two compares:
+// log_alpha_t is la = A + (H + g) (birth, death) or A + g (change) or g (move), g = (phi - phi_n) * inv_2t;
+// la0 = la at g = 0, as log_alpha_t forms it, and mag = |A| + 2|H| bound the rounding:
+//     |la_fp(g) - (la0 + g)| <= 3u (|la0| + mag + 2|g|)     (u = 2^-53)
+// so decide_sure() answers only where log_u < la_fp at every point of the bracket (1: accept) or at
+// none (-1: reject), with a margin of 2^-45 relative -- else 0, and the caller evaluates the bracket's
+// corners with accept_t.  (la_fp is monotone in g and g in phi, phi_n: each IEEE step is.)
+struct AlphaParts {
+    double la0, mag;
+    int reject;  // accept_t rejects whatever phi, phi_n (an invalid proposal; an exponential death at zetanew <= 0)
+};
+TD_HD AlphaParts alpha_parts(const Params &P, const Proposal &p, double czeta, double zeta_killed,
+                             double zetanew_death, const double *lnN) {
+    AlphaParts r;
+    r.reject = !p.active || !p.valid || (p.action == kDeath && P.prior == kExponential && !(zetanew_death > 0.0));
+    r.la0 = log_alpha_t(P, 1.0, p, 0.0, 0.0, czeta, zeta_killed, zetanew_death, lnN);  // g = 0
+    double A = 0.0, H = 0.0;
+    if (p.action == kBirth) {
+        const double dz = czeta - p.zeta;
+        H = (dz * dz) * P.inv_2sig2;
+        if (P.prior == kNormal) H = -(p.zeta * p.zeta) * P.inv_zs2 + H;
+        else if (P.prior == kExponential) H = -p.zeta * P.inv_zs + H;
+        A = (lnN[1] - lnN[2]) + P.log_prior_birth;
+    } else if (p.action == kDeath) {
+        const double dz = zeta_killed - zetanew_death;
+        H = -((dz * dz) * P.inv_2sig2);
+        if (P.prior == kNormal) H = (zeta_killed * zeta_killed) * P.inv_2zs2 + H;
+        else if (P.prior == kExponential) H = zeta_killed * P.inv_zs + H;
+        A = (lnN[1] - lnN[0]) + P.log_prior_death;
+    } else {
+        A = r.la0;  // change: A + g; move: g (la0 = 0)
+    }
+    r.mag = fabs(A) + 2.0 * fabs(H);
+    return r;
+}
+// 1: accept_t accepts for every g >= g_lo; -1: for no g <= g_hi; 0: undecided (g_lo <= g_hi)
+TD_HD int decide_sure(const AlphaParts &a, double log_u, double g_lo, double g_hi) {
+    if (a.reject) return -1;
+    const double lo = a.la0 + g_lo, hi = a.la0 + g_hi;
+    const double tl = 0x1p-45 * (fabs(a.la0) + a.mag + 2.0 * fabs(g_lo) + fabs(lo) + fabs(log_u));
+    const double th = 0x1p-45 * (fabs(a.la0) + a.mag + 2.0 * fabs(g_hi) + fabs(hi) + fabs(log_u));
+    if (lo - tl > log_u) return 1;  // (NaN, infinities: every comparison false -> undecided)
+    if (hi + th < log_u) return -1;
+    return 0;
+}
+
 // The phi_n from which accept() rejects: log_alpha is dphi-affine, so
 //     reject  <=>  phi_n >= phi + 2T (log f + g - log u)
 // (f, g as in log_alpha).  For deciding before phi_n is known exactly (the

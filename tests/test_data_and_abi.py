@@ -268,6 +268,46 @@ def test_acceptance_matches_reference_formulas(tt):
 
 
 
+def test_decision_prefilter_is_sound(tt):
+    """The device decides most proposals from the phi-free part of log alpha and one add (chain_logic.h
+    decide_sure) before it evaluates the acceptance rule at the corners of its (phi, phi_n) brackets.  Its
+    answer must be the rule's at every point of the bracket: checked on brackets of 1e-16 .. 1e-3
+    relative width placed at random and straddling the rule's own threshold (found by bisection)."""
+    L = tt.lib()
+    rng = np.random.default_rng(11)
+    decided = total = 0
+    for prior in (1, 2, 3):
+        for T in (1.0, 3.0):
+            prm = params(tt, temperature=T, prior=prior)
+            for _ in range(400):
+                action = int(rng.integers(1, 5))
+                N = int(rng.integers(6, 99))
+                phi = rng.uniform(100, 900)
+                cz, zn, zk, zd = rng.uniform(-10, 60, 4) if prior != 1 else rng.uniform(0, 50, 4)
+                u = rng.uniform()
+                acc = lambda pn, ph=phi: L.tdt_accept(ctypes.byref(prm), action, u, zn, N, ph, pn, cz, zk, zd)
+                lo, hi = phi - 200.0, phi + 200.0  # the rule's threshold in phi_n, if inside
+                if acc(lo) and not acc(hi):
+                    for _ in range(80):
+                        mid = 0.5 * (lo + hi)
+                        lo, hi = (mid, hi) if acc(mid) else (lo, mid)
+                centers = [lo, hi, phi + rng.normal(0, 6)]
+                for ci, c in enumerate(centers):
+                    for rel in (1e-16, 1e-12, 1e-9, 1e-6, 1e-3):
+                        w = abs(c) * rel * rng.uniform(0.5, 2.0)
+                        a, b = c - w * rng.uniform(), c + w * rng.uniform()
+                        p_lo, p_hi = phi * (1 - rel * rng.uniform()), phi * (1 + rel * rng.uniform())
+                        r = L.tdt_decide_sure(ctypes.byref(prm), action, u, zn, N, p_lo, p_hi, a, b, cz, zk, zd)
+                        total += ci == 2
+                        if r == 1:  # accepted at the bracket's worst corner, hence everywhere
+                            decided += ci == 2
+                            assert acc(b, p_lo) == 1 and acc(a, p_hi) == 1, (prior, action, c, rel)
+                        elif r == -1:
+                            decided += ci == 2
+                            assert acc(a, p_hi) == 0 and acc(b, p_lo) == 0, (prior, action, c, rel)
+    assert decided > 0.9 * total  # (brackets placed at random: nearly all decided without the corners)
+
+
 def test_td_info_layout_matches_header():
     """td_info (include/tdstar.h) and the ctypes mirror agree: the ABI version and
     the struct's size (num_cus appended in ABI 2)."""
