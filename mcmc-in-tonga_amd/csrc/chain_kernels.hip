@@ -262,6 +262,7 @@ struct Shared {
     int ob_lo[3], ob_hi[3], ob_ncand, ob_nfb;  // phase D's orphan-batch search (LDS layout)
     int n_super[2];  // rays in HBM: super-tiles hit, by iteration parity (the next iteration refreshes their maxima)
     int pts_seen, ray_pts;
+    int e_done;  // LDS layout: waves done with their phase-E rays (waves 1..; wave 0 waits for them)
     // bucket-grid update of an accepted proposal (applied by the last wave in phase G)
     int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site, bit 4: new value in place
     // what the update needs from the grid, read during phase F (G only writes)
@@ -1319,6 +1320,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         sh.defer = 0;
         if (!RLDS) sh.dsum = sh.dabs = 0.0;
         sh.grid_fallbacks32 = 0;
+        sh.e_done = 0;
         geo_fill(sh.geo, d);
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
@@ -1937,7 +1939,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         atomicAdd(&sh.dsum, nterm - old_term);
                         atomicAdd(&sh.dabs, fabs(nterm) + fabs(old_term));
                     }
-                    atomicAdd(&sh.ray_pts, npr);
+                    if constexpr (RLDS)  // (the accounting below may run before phase E is over)
+                        atomicAdd((unsigned long long *)&sh.bytes, (unsigned long long)npr * 17ull);
+                    else
+                        atomicAdd(&sh.ray_pts, npr);
                     if constexpr (WALK)  // an event of the walk (scripted steps: the decisions on bounds need none)
                         if (nscript) atomicOr(&cmask[r >> 6], 1ull << (r & 63));
                 };
@@ -2017,8 +2022,22 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         const double val = wave_ray_sum(lane, d.w, oz, s0, npr, ray_scratch[wv]);
                         if (lane == 0) ray_done(r, val, tsr, sgr, old_term, npr);
                     }
+                    if constexpr (RLDS) {
+                        // no block barrier after phase E: only wave 0's decision reads the new terms, so a
+                        // wave that summed rays counts itself done (its LDS writes first) and wave 0 waits
+                        // for those (~1.2 rays a proposal: mostly none); the other waves go straight on to
+                        // phase F's side work
+                        if (wv != 0 && wv < nr) {
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            if (lane == 0) atomicAdd(&sh.e_done, 1);
+                        } else if (wv == 0 && nr > 1) {
+                            const int want = min(nr, kWv) - 1;
+                            while (__hip_atomic_load(&sh.e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+                                __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
                 }
-                __syncthreads();
+                if constexpr (!RLDS) __syncthreads();
                 STAMP(4);
             }
             // a server's step decided later: its answer goes out now, before phase F -- the changed rays'
@@ -2231,7 +2250,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                                                  : (long long)NT * 32) +
                                                        (long long)sh.pts_seen * 36 +
                                                        (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
-                                                       (long long)sh.ray_pts * 17 + (long long)(n - sh.k0) * 28));
+                                                       (RLDS ? 0ll : (long long)sh.ray_pts * 17) + (long long)(n - sh.k0) * 28));
                     }
                     if (lane == 0 && (action == tdchain::kBirth || action == tdchain::kDeath)) {
                         sh.lnN_far[0] = d.logN[max(ncells - 2, 0)];
@@ -2521,6 +2540,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     if (!RLDS) sh.dsum = sh.dabs = 0.0;
                     sh.n_super[(it + 1) & 1] = 0;  // the other parity's list is refreshed first
                     sh.pts_seen = sh.ray_pts = 0;
+                    sh.e_done = 0;
                     sh.k0 = n;
                     sh.accept = 0;
                 }
