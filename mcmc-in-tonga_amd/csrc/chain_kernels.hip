@@ -263,6 +263,7 @@ struct Shared {
     int n_super[2];  // rays in HBM: super-tiles hit, by iteration parity (the next iteration refreshes their maxima)
     int pts_seen, ray_pts;
     int e_done;  // LDS layout: waves done with their phase-E rays (waves 1..; wave 0 waits for them)
+    int b_done;  // LDS layout: waves done with their phase-B tile pass (phase B without its barrier)
     // bucket-grid update of an accepted proposal (applied by the last wave in phase G)
     int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site, bit 4: new value in place
     // what the update needs from the grid, read during phase F (G only writes)
@@ -1189,6 +1190,7 @@ template <bool SMALL, bool SCRIPT, int NTH, bool RLDS = SMALL, bool ROUNDS = fal
 __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict__ dptr, long long iters,
                                                              ScriptArgs sa) {
     constexpr bool WALK = !SMALL || kSmallWalk;  // chi^2 by the event walk
+    constexpr bool kNoBarB = RLDS && !SCRIPT;     // phase B may end without a block barrier (below)
     constexpr int kWv = NTH / 64;  // waves: 8 (one chain per CU), or 4 (rays in HBM: two chains per CU)
     static_assert(!RLDS || SMALL, "rays in LDS only with the tiles in LDS");
     static_assert(NTH == kChainThreads || (!RLDS && !SCRIPT && NTH == kChainThreads / 2),
@@ -1320,7 +1322,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         sh.defer = 0;
         if (!RLDS) sh.dsum = sh.dabs = 0.0;
         sh.grid_fallbacks32 = 0;
-        sh.e_done = 0;
+        sh.e_done = sh.b_done = 0;
         geo_fill(sh.geo, d);
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
@@ -1505,6 +1507,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         // phase B (their global round trip overlaps the B barrier and the birth/death
         // query) and judged in phase C
         bool pre_on = false;
+        bool nobar = false;  // phase B without its block barrier (block-uniform; below)
         int pre_q = 0, pre_ray = 0, pre_s = 0;
         double pre_bd = 0.0, pre_x = 0.0, pre_y = 0.0, pre_z = 0.0;
         if (p.active) {
@@ -1514,6 +1517,12 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             // (TD_inversion_function.jl:146): the idle query wave answers it here, posted with the report)
             const bool kill_q = SCRIPT && mb && action == tdchain::kDeath && sh.step_cur.decision == kDecideLater;
             const bool query = (!nscript && (action == tdchain::kBirth || action == tdchain::kDeath)) || kill_q;
+            // LDS layout, free-running, no birth: phase B ends without a block barrier.  Phase C needs of
+            // the tile pass only each wave's own first hit tiles (their points are in its registers) until
+            // it walks the whole hit list: each wave counts itself done after its tile pass (a death's
+            // query wave before its query, whose answer only the decision reads) and a wave waits for all
+            // of them after its own points.  (A birth's marks need the query's answer: the barrier stays.)
+            nobar = kNoBarB && action != tdchain::kBirth && p.valid && P.debug_prior != 1;
             if (eval) {
                 // tiles whose box can hold a point the proposal changes (the last
                 // wave answers the Interpolation query meanwhile)
@@ -1647,6 +1656,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                     }
             }
+            if (nobar && !(query && wv == kWv - 1)) {  // (every wave but the query wave: its tile pass is done)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) atomicAdd(&sh.b_done, 1);
+            }
             if (RLDS && action == tdchain::kDeath && nscript) {  // deleteat! shift, staged before we know if it is accepted
                 const int sthr = query ? NTH - 64 : NTH;  // not the query wave: it starts at once
                 // (the order in HBM: no staging -- an accepted death shifts it in phase G)
@@ -1657,13 +1670,16 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             }
             if (query && wv == kWv - 1) {  // TD_inversion_function.jl:81 (birth), :146 (death)
                 const bool birth = action == tdchain::kBirth;
+                if (nobar && lane == 0) atomicAdd(&sh.b_done, 1);  // (a death: nothing in phase C waits for this query)
                 const Nearest r = wave_nearest(d, v, sh, lane, birth ? p.x : kx, birth ? p.y : ky, birth ? p.z : kz,
                                                birth ? -1 : slot_k, -1, 0.0, 0.0, 0.0, 0.0);
                 if (lane == 0) sh.q_zeta = r.z;
             }
-            __syncthreads();  // tile list complete, query answered
-            if (action == tdchain::kBirth) czeta = sh.q_zeta;
-            if (action == tdchain::kDeath) zetanew_death = sh.q_zeta;
+            if (!nobar) {
+                __syncthreads();  // tile list complete, query answered
+                if (action == tdchain::kBirth) czeta = sh.q_zeta;
+                if (action == tdchain::kDeath) zetanew_death = sh.q_zeta;
+            }
         }
         Proposal pp = p;
         if (p.active && action == tdchain::kBirth && !nscript) tdchain::birth_zeta(P, pp, czeta);  // every lane, same value
@@ -1676,7 +1692,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             if (fwd) {
                 // ================= phase C: affected points =================
                 if (!nscript && tid == NTH - 64)  // the decision's phi-free part, off phase F's path
-                    sh.ap = tdchain::alpha_parts(P, pp, czeta, zeta_killed, zetanew_death, sh.lnN);
+                    sh.ap = tdchain::alpha_parts(P, pp, czeta, zeta_killed,
+                                                 nobar && action == tdchain::kDeath ? sh.q_zeta : zetanew_death,
+                                                 sh.lnN);  // (nobar: this lane asked the death's query itself)
 
                 const int nt = sh.n_tiles;
                 // the selected cell's value, known since the proposal was made: czeta[slot_k] = zeta_killed
@@ -1706,6 +1724,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         ++seen;
                         point(pre_q, pre_ray, pre_s, pre_bd, pre_x, pre_y, pre_z);
                     }
+                    if (nobar)  // the whole hit list from here on: every wave's tile pass done
+                        while (__hip_atomic_load(&sh.b_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kWv)
+                            __builtin_amdgcn_s_sleep(1);
+                    const int nt = sh.n_tiles;
                     for (int item = tid; item < nt * kTilePts; item += NTH) {
                         const int t = v.thit[item / kTilePts];
                         if (t < 0) continue;  // preloaded
@@ -1749,6 +1771,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 }
                 if (seen) atomicAdd(&sh.pts_seen, seen);
                 __syncthreads();
+                if (nobar && action == tdchain::kDeath) zetanew_death = sh.q_zeta;  // (the query wave is past it)
                 STAMP(2);
                 // ========= phase D: re-search orphaned points, one wave each =========
                 no = sh.n_orphans;
@@ -2540,7 +2563,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     if (!RLDS) sh.dsum = sh.dabs = 0.0;
                     sh.n_super[(it + 1) & 1] = 0;  // the other parity's list is refreshed first
                     sh.pts_seen = sh.ray_pts = 0;
-                    sh.e_done = 0;
+                    sh.e_done = sh.b_done = 0;
                     sh.k0 = n;
                     sh.accept = 0;
                 }
