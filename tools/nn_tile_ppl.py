@@ -1,5 +1,6 @@
 """k_nn_tile alone (tdt_nn_bench, back-to-back launches) at the config-3 point set for 200 / 1000 / 5000 /
-20000 cells, under the points-per-lane of TD_NN_PPL (run once per value: the choice is read once)."""
+20000 cells.  (profiles/r05/nn_tile/ holds the sweep over 2 / 3 / 4 points per lane taken with a TD_NN_PPL
+knob of the library, removed after it: 2 per lane stays.)"""
 import ctypes
 import json
 import os
