@@ -582,3 +582,42 @@ def test_hbm_layout_edge_rays_follow_host_engine(tt):
     dev.close()
     host.close()
     c2.close()
+
+
+@pytest.mark.parametrize("clustered", [False, True])
+def test_grid_query_forms_agree(tt, ds, ctx, clustered):
+    """The chain's grid query reads the grid from its LDS copy and proves its answer first against the
+    global bound (h - 2e)^2 (GridGeo); the descriptor-reading form with the query's own face bound
+    is kept for comparison (tdt_chain_query_lat modes 0 and 6).  Both must give the same (distance,
+    slot, proven) for every query: ray points, points spread over the cells' box and beyond it, and
+    (clustered) cells packed into one spot plus exact duplicates, where buckets overflow."""
+    rng = np.random.default_rng(9 if clustered else 8)
+    if clustered:
+        xmin, xmax, ymin, ymax, zmin, zmax = tt.box()
+        k = 300
+        x = np.concatenate([rng.uniform(400, 402, k), rng.uniform(xmin, xmax, 200)])
+        y = np.concatenate([rng.uniform(100, 102, k), rng.uniform(ymin, ymax, 200)])
+        z = np.concatenate([rng.uniform(300, 302, k), rng.uniform(zmin, zmax, 200)])
+        x[7], y[7], z[7] = x[6], y[6], z[6]
+        model = tt.Model(float(len(x)), x, y, z, rng.uniform(1, 49, len(x)))
+    else:
+        model = tt.random_model(5000, 3)
+    prm = tt.define_TDstructrure().replace(max_cells=10000)
+    ch = make(tt, ctx, prm, model, 23, tt.TD_ENGINE_DEVICE)
+    ch.run(300)
+    X, Y, Z = (np.asarray(a, dtype=np.float64).ravel() for a in (ds.rayX, ds.rayY, ds.rayZ))
+    ok = ~np.isnan(X)
+    X, Y, Z = X[ok], Y[ok], Z[ok]
+    sel = rng.integers(0, len(X), 1500)
+    lo, hi = np.array([X.min(), Y.min(), Z.min()]), np.array([X.max(), Y.max(), Z.max()])
+    box = lo - 50.0 + (hi - lo + 100.0) * rng.random((1500, 3))
+    pts = np.ascontiguousarray(np.concatenate([np.stack([X[sel], Y[sel], Z[sel]], 1), box]), dtype=np.float64)
+    L = tt.lib()
+    digests = []
+    for mode in (0, 6):
+        out = (ctypes.c_int64 * 4)()
+        assert L.tdt_chain_query_lat(ch.h, pts.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(pts), mode,
+                                     out) == 0
+        digests.append(out[3])
+    assert digests[0] == digests[1]
+    ch.close()
