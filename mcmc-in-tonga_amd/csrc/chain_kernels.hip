@@ -2559,6 +2559,11 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     const tdchain::Proposal &np = sh.ps[cur_r].p;
                     if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
                     sh.spec_ok = 0;
+                    // (the other waves read these counters and sh.accept as their first instructions after
+                    // phase F's barrier; this lane gets here through its whole commit and this block, over a
+                    // thousand cycles of dependent LDS work later, on instructions every wave has just
+                    // fetched.  A count of the waves' reads for this lane to wait on measured -2 %, reading
+                    // them before the barrier -3 % -- register allocation -- and is not kept)
                     sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
                     if (!RLDS) sh.dsum = sh.dabs = 0.0;
                     sh.n_super[(it + 1) & 1] = 0;  // the other parity's list is refreshed first
