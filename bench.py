@@ -105,6 +105,10 @@ def chain_roofline(kernel, ref_bytes_per_proposal, proposals_per_launch, avg_lau
            "incremental_achieved": round(inc, 3), "incremental_frac": round(inc / HBM_PEAK_GBS, 6),
            "proposals_per_launch": proposals_per_launch, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
            "us_per_proposal": round(avg_launch_s / max(proposals_per_launch, 1) * 1e6, 4)}
+    if achieved > HBM_PEAK_GBS:  # (many chains: one evaluate per proposal could not run at this rate)
+        out["note"] = ("frac > 1: the reference's one-evaluate-per-proposal bytes at this proposal rate exceed the "
+                       "HBM peak; the incremental proposals read incremental_achieved, the PMC-measured HBM bytes "
+                       "are traffic")
     if match:
         tr, src, prof_us = measured_traffic(traffic_key)
         if tr is not None:
