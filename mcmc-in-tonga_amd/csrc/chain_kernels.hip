@@ -332,6 +332,24 @@ __device__ __forceinline__ void shift_range(int index, int ncells, int w, int nw
         }                                          \
     } while (0)
 
+// Wave-skew testing build (-DTD_CHAIN_SKEW, tools/build_skew.sh): after every block barrier and every
+// barrier-free phase end of the chain loop, one wave -- rotating with the iteration and the site --
+// sleeps 8k-16k cycles (a whole phase or more), so any shared word read without a synchronisation
+// that orders it shows up as a wrong answer in the chain parity tests.  Off in the product build.
+#ifdef TD_CHAIN_SKEW
+#define SKEW(site)                                                                      \
+    do {                                                                                \
+        if (wv == (int)(((unsigned long long)it * 5ull + (site)) % (unsigned)kWv)) {    \
+            __builtin_amdgcn_s_sleep(127);                                              \
+            if (((it + (site)) & 1) != 0) __builtin_amdgcn_s_sleep(127);                \
+        }                                                                               \
+    } while (0)
+#else
+#define SKEW(site) \
+    do {           \
+    } while (0)
+#endif
+
 // LDS carve-up (host and device agree on it through this function).
 struct LdsPlan {
     size_t scratch, draws, smask, cmask, slo, shi, smax, shit, hrec, rhitl, tlo, thi, tmaxd, tstart, thit, ctm, tray, rayoff, ptS, prefix, cptS, cprefix, term, cterm,
@@ -1488,6 +1506,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     if ((tid & 15) == 15) smax[S] = f32_up(__longlong_as_double((long long)mk));
                 }
                 __syncthreads();
+                SKEW(1);
                 pend_sup = false;
             }
         }
@@ -1555,6 +1574,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                 }
                         }
                     __syncthreads();  // (the query wave too: it starts its query after this)
+                    SKEW(2);
                     const int nsh = sh.n_super[par];
                     const bool all = nsh > kListLds;  // the list overflowed: every tile
                     const int nitems = all ? NS * kTilePts : nsh * kTilePts;
@@ -1659,6 +1679,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             if (nobar && !(query && wv == kWv - 1)) {  // (every wave but the query wave: its tile pass is done)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == 0) atomicAdd(&sh.b_done, 1);
+                SKEW(3);
             }
             if (RLDS && action == tdchain::kDeath && nscript) {  // deleteat! shift, staged before we know if it is accepted
                 const int sthr = query ? NTH - 64 : NTH;  // not the query wave: it starts at once
@@ -1677,6 +1698,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             }
             if (!nobar) {
                 __syncthreads();  // tile list complete, query answered
+                SKEW(4);
                 if (action == tdchain::kBirth) czeta = sh.q_zeta;
                 if (action == tdchain::kDeath) zetanew_death = sh.q_zeta;
             }
@@ -1771,6 +1793,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 }
                 if (seen) atomicAdd(&sh.pts_seen, seen);
                 __syncthreads();
+                SKEW(5);
                 if (nobar && action == tdchain::kDeath) zetanew_death = sh.q_zeta;  // (the query wave is past it)
                 STAMP(2);
                 // ========= phase D: re-search orphaned points, one wave each =========
@@ -1813,6 +1836,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             sh.ob_ncand = sh.ob_nfb = 0;
                         }
                         __syncthreads();
+                        SKEW(6);
                         for (int o = tid; o < no; o += NTH) {
                             double qx, qy, qz;
                             orphan_xyz(o, qx, qy, qz);
@@ -1826,6 +1850,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             atomicMax(&sh.ob_hi[2], bk);
                         }
                         __syncthreads();
+                        SKEW(7);
                         const int i0 = max(sh.ob_lo[0] - 1, 0), i1 = min(sh.ob_hi[0] + 1, G.gx - 1);
                         const int j0 = max(sh.ob_lo[1] - 1, 0), j1 = min(sh.ob_hi[1] + 1, G.gy - 1);
                         const int k0b = max(sh.ob_lo[2] - 1, 0), k1b = min(sh.ob_hi[2] + 1, G.gz - 1);
@@ -1845,6 +1870,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                 }
                             }
                             __syncthreads();
+                            SKEW(8);
                             const int nc = sh.ob_ncand;
                             if (nc <= kBatchCand) {
                                 // four lanes per orphan (a quad), each over a quarter of the entries,
@@ -1918,6 +1944,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                     }
                                 }
                                 __syncthreads();
+                                SKEW(9);
                                 nlist = sh.ob_nfb;
                                 olist = fb;
                             }
@@ -1946,6 +1973,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     if (lane == 0) mark(d, v, sh, q, ray, r.s, r.d, r.z);
                 }
                 if (nlist > 0) __syncthreads();
+                SKEW(10);
                 STAMP(3);
                 // ================= phase E: t* of the rays that changed =================
                 const int nr = sh.n_rays;
@@ -2058,9 +2086,11 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             while (__hip_atomic_load(&sh.e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
                                 __builtin_amdgcn_s_sleep(1);
                         }
+                        SKEW(11);
                     }
                 }
                 if constexpr (!RLDS) __syncthreads();
+                SKEW(12);
                 STAMP(4);
             }
             // a server's step decided later: its answer goes out now, before phase F -- the changed rays'
@@ -2114,6 +2144,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     const double wsum = wave_sum_f64((p0 + p1) + (p2 + p3));
                     if (lane == 0) sh.wpart[wv] = wsum;
                     __syncthreads();
+                    SKEW(13);
                 }
             }
             if (RLDS && !nscript && action == tdchain::kDeath && lane == 0) {  // what phase G's shift overwrites
@@ -2332,6 +2363,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 atomicAdd((unsigned long long *)&sh.prof[56 + wv], (unsigned long long)(clock64() - tF));
             __syncthreads();
             STAMP(5);
+            SKEW(14);
             // ================= phase G: commit (or undo) =================
             const int nc = sh.n_changed, nr = sh.n_rays;
             const int sdec = nscript ? sh.step_cur.decision : 1;
@@ -2339,6 +2371,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             if (mb && sdec == kDecideLater) {  // answered before phase F; its fate comes with the next command
                 if (wv == 0) server_wait(mb, d, v, sh, lane);
                 __syncthreads();
+                SKEW(15);
                 if (tid == 0) acc_r = sh.accept != 0;
             }
             // the changed points' global records (two dependent L2 round trips) and the
@@ -2397,6 +2430,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         __builtin_amdgcn_s_waitcnt(0);
                         atomicAdd(&sh.shift_done, 1);
                     }
+                    SKEW(16);
                 }
                 if (RLDS && action == tdchain::kDeath && wv != 0 && nscript) {  // deleteat!: from the staged copy
                     constexpr int U = 4;                                 // U loads in flight per thread
@@ -2475,6 +2509,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
 #pragma unroll
                             for (int u = 0; u < U; ++u) sl[u] = gload(v.ord + min(b0 + tid + u * NTH, ncells - 1));
                             __syncthreads();
+                            SKEW(18);
 #pragma unroll
                             for (int u = 0; u < U; ++u) {
                                 const int j = b0 + tid + u * NTH;
@@ -2578,6 +2613,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         it_done = it + 1;
         __syncthreads();
         STAMP(6);
+        SKEW(17);
     }
 
     const long long t_loop_end = prof_on ? clock64() : 0;
