@@ -46,6 +46,11 @@ int tdt_chain_lds(td_chain *ch, int64_t out[4]);
  * (pts: nq x {x, y, z}); mode 0: the whole query, 1: its loads only, 2: its arithmetic only.
  * out[0] = cycles, out[1] = unproven queries (full scans). */
 int tdt_chain_query_lat(td_chain *ch, const double *pts, int nq, int mode, int64_t out[4]);
+/* Each query's answer from the chain's grid search (mode 0: the LDS grid copy with the global first
+ * bound; 6: the descriptor-reading form): squared distance, the winning cell's value, proven (1) or
+ * left to the full scan (0). */
+int tdt_chain_query_answers(td_chain *ch, const double *pts, int nq, int mode, double *dist, double *value,
+                            int32_t *proven);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */
 int tdt_accept(const td_chain_params *prm, int action, double u_accept, double zeta_new, int64_t ncells, double phi,
                double phi_n, double czeta, double zeta_killed, double zetanew_death);

@@ -95,6 +95,7 @@ SIGNATURES = {
     "tdt_chain_profile": (ctypes.c_int, [_vp, ctypes.c_int, _pi64]),
     "tdt_chain_lds": (ctypes.c_int, [_vp, _pi64]),
     "tdt_chain_query_lat": (ctypes.c_int, [_vp, _pd, ctypes.c_int, ctypes.c_int, _pi64]),
+    "tdt_chain_query_answers": (ctypes.c_int, [_vp, _pd, ctypes.c_int, ctypes.c_int, _pd, _pd, _pi32]),
     "tdt_set_nn_method": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_nn_bench": (ctypes.c_int, [_vp, _pd, _pd, _pd, _pd, _i64, ctypes.c_int, ctypes.c_int, _pd]),
     "tdt_chain_set_lds_mode": (ctypes.c_int, [_vp, ctypes.c_int]),

@@ -1856,6 +1856,35 @@ int tdt_chain_query_lat(td_chain *ch, const double *pts, int nq, int mode, int64
     return TD_OK;
 }
 
+int tdt_chain_query_answers(td_chain *ch, const double *pts, int nq, int mode, double *dist, double *value,
+                            int32_t *proven) {
+    if (!ch || ch->engine != TD_ENGINE_DEVICE || !pts || nq < 1 || !dist || !value || !proven ||
+        (mode != 0 && mode != 6))
+        return TD_ERR_ARG;
+    td_ctx *c = ch->ctx;
+    double *dp = nullptr, *dd = nullptr, *dz = nullptr;
+    int *dpr = nullptr;
+    const size_t n = (size_t)nq;
+    hipError_t e = hipMalloc((void **)&dp, sizeof(double) * 3 * n);
+    if (e == hipSuccess) e = hipMalloc((void **)&dd, sizeof(double) * n);
+    if (e == hipSuccess) e = hipMalloc((void **)&dz, sizeof(double) * n);
+    if (e == hipSuccess) e = hipMalloc((void **)&dpr, sizeof(int) * n);
+    if (e == hipSuccess) e = hipMemcpy(dp, pts, sizeof(double) * 3 * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && ch->desc_dirty) {
+        e = hipMemcpy(ch->dev_ptr, &ch->dev, sizeof(DevChain), hipMemcpyHostToDevice);
+        ch->desc_dirty = false;
+    }
+    if (e == hipSuccess) e = test_query_answers(ch->dev_ptr, dp, nq, mode, dd, dz, dpr, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(dist, dd, sizeof(double) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(value, dz, sizeof(double) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(proven, dpr, sizeof(int) * n, hipMemcpyDeviceToHost);
+    for (void *q : {(void *)dp, (void *)dd, (void *)dz, (void *)dpr})
+        if (q) (void)hipFree(q);
+    if (e != hipSuccess) return hip_err(c, e, "tdt_chain_query_answers");
+    return TD_OK;
+}
+
 int tdt_chain_profile(td_chain *ch, int enable, int64_t out[80]) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE) return TD_ERR_ARG;
     ch->dev.profile = enable;

@@ -24,6 +24,31 @@ def test_bench_spawns_its_ranks(n):
     assert len(lines) == 1, p.stdout  # rank 0 alone prints
     out = json.loads(lines[0])
     assert out["n_gpus"] == n and out["ranks_seen"] == n
+    assert out["leg_check"] == {"ranks": n}  # a multi-rank leg under run_leg's deadline
+
+
+@pytest.mark.timeout(240)
+def test_stalled_leg_still_prints_the_line():
+    """A rank that never joins a multi-rank leg's collective: rank 0 prints
+    the line (everything measured before the leg) with that leg as a deadline
+    error when the ranks' agreed deadline passes, and the run exits non-zero
+    instead of hanging until the driver's limit (bench.run_leg)."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["TD_BENCH_STALL_LEG"] = "leg_check:1"
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
+                        "--leg-deadline", "8"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=220,
+                       cwd=ROOT)
+    el = time.time() - t0
+    assert p.returncode != 0, p.stderr.decode(errors="replace")[-3000:]
+    lines = [x for x in p.stdout.decode().splitlines() if x.startswith("{")]
+    assert len(lines) == 1, (p.stdout, p.stderr.decode(errors="replace")[-3000:])
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks_seen"] == 2
+    assert out["leg_check"]["error"] == "deadline"
+    assert el < 8 + 100  # the deadline, not the process group's 120 s timeout
 
 
 @pytest.mark.timeout(120)

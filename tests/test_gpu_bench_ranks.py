@@ -55,3 +55,32 @@ def test_bench_two_ranks_gloo(launcher):
     assert sc["chains"] == 2 and sc["proposals_per_s"] > 0
     assert sc["roofline"]["bound"] == "latency" and sc["roofline"]["achieved"] > 0
     assert "stress_sharded" in out
+
+
+@pytest.mark.timeout(300)
+def test_bench_stalled_leg_prints_headline():
+    """The driver's N-GPU run must not hang silently on a multi-rank leg: rank 1
+    stalls in the config-4 leg (TD_BENCH_STALL_LEG) before its first collective;
+    when the ranks' agreed deadline passes, rank 0 prints ONE line with the
+    headline already measured, config4_ranks as a deadline error and the later
+    legs as skipped, and the run exits non-zero (bench.run_leg)."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(TD_BENCH_BACKEND="gloo", TD_BENCH_DEVICE="0", TD_BENCH_STALL_LEG="config4_ranks:1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--iters-per-step", "500", "--no-cpu-baseline", "--no-full-evaluate", "--no-dropin", "--batch-chains", "0",
+           "--config4-rounds", "40", "--stress-iters", "100", "--no-phases", "--leg-deadline", "20"]
+    t0 = time.time()
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=280, cwd=ROOT)
+    el = time.time() - t0
+    text = p.stdout.decode(errors="replace")
+    assert p.returncode != 0, text[-4000:]
+    lines = [x for x in text.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, text[-4000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["roofline"]["frac"] <= 1.0
+    assert out["config4_ranks"]["error"] == "deadline", out["config4_ranks"]
+    assert out["stress_chains"]["error"].startswith("skipped") and out["stress_sharded"]["error"].startswith("skipped")
+    assert el < 250

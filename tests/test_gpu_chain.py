@@ -585,12 +585,16 @@ def test_hbm_layout_edge_rays_follow_host_engine(tt):
 
 
 @pytest.mark.parametrize("clustered", [False, True])
-def test_grid_query_forms_agree(tt, ds, ctx, clustered):
+def test_grid_query_forms_agree(tt, ds, ctx, orc, clustered):
     """The chain's grid query reads the grid from its LDS copy and proves its answer first against the
     global bound (h - 2e)^2 (GridGeo); the descriptor-reading form with the query's own face bound
     is kept for comparison (tdt_chain_query_lat modes 0 and 6).  Both must give the same (distance,
-    slot, proven) for every query: ray points, points spread over the cells' box and beyond it, and
-    (clustered) cells packed into one spot plus exact duplicates, where buckets overflow."""
+    slot, proven) for every query: ray points, points spread over the cells' box and far beyond it,
+    the live cells' own sites (distance 0; exact duplicates tie), and (clustered) cells packed into
+    one spot plus exact duplicates, where buckets overflow.  And every answer either form calls proven
+    must be the exact one: v_nearest's first minimum over the live cells in Julia order
+    (MCsub.jl:247-263, the C oracle's interpolation), distance and value bit for bit -- so a bound
+    shared by both forms (the sealed box, the global first bound) is checked against a full scan."""
     rng = np.random.default_rng(9 if clustered else 8)
     if clustered:
         xmin, xmax, ymin, ymax, zmin, zmax = tt.box()
@@ -599,6 +603,7 @@ def test_grid_query_forms_agree(tt, ds, ctx, clustered):
         y = np.concatenate([rng.uniform(100, 102, k), rng.uniform(ymin, ymax, 200)])
         z = np.concatenate([rng.uniform(300, 302, k), rng.uniform(zmin, zmax, 200)])
         x[7], y[7], z[7] = x[6], y[6], z[6]
+        x[k + 5], y[k + 5], z[k + 5] = x[k + 4], y[k + 4], z[k + 4]
         model = tt.Model(float(len(x)), x, y, z, rng.uniform(1, 49, len(x)))
     else:
         model = tt.random_model(5000, 3)
@@ -611,13 +616,32 @@ def test_grid_query_forms_agree(tt, ds, ctx, clustered):
     sel = rng.integers(0, len(X), 1500)
     lo, hi = np.array([X.min(), Y.min(), Z.min()]), np.array([X.max(), Y.max(), Z.max()])
     box = lo - 50.0 + (hi - lo + 100.0) * rng.random((1500, 3))
-    pts = np.ascontiguousarray(np.concatenate([np.stack([X[sel], Y[sel], Z[sel]], 1), box]), dtype=np.float64)
+    far = lo - 1000.0 + (hi - lo + 2000.0) * rng.random((300, 3))  # well outside the cells' box too
+    m = ch.model()
+    cells = np.stack([m.xCell, m.yCell, m.zCell], 1)
+    sites = cells[rng.integers(0, len(cells), 200)]
+    pts = np.ascontiguousarray(np.concatenate([np.stack([X[sel], Y[sel], Z[sel]], 1), box, far, sites]),
+                               dtype=np.float64)
     L = tt.lib()
+    P = ctypes.POINTER(ctypes.c_double)
     digests = []
     for mode in (0, 6):
         out = (ctypes.c_int64 * 4)()
-        assert L.tdt_chain_query_lat(ch.h, pts.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(pts), mode,
-                                     out) == 0
+        assert L.tdt_chain_query_lat(ch.h, pts.ctypes.data_as(P), len(pts), mode, out) == 0
         digests.append(out[3])
     assert digests[0] == digests[1]
+    # the proven answers against the exact scan (every live cell, Julia order, first minimum)
+    val, ids = orc.interpolation(m.cells(), pts[:, 0], pts[:, 1], pts[:, 2])
+    dx, dy, dz = (pts[:, 0] - m.xCell[ids]), (pts[:, 1] - m.yCell[ids]), (pts[:, 2] - m.zCell[ids])
+    dref = (dx * dx + dy * dy) + dz * dz
+    for mode in (0, 6):
+        dist, value = np.zeros(len(pts)), np.zeros(len(pts))
+        proven = np.zeros(len(pts), dtype=np.int32)
+        assert L.tdt_chain_query_answers(ch.h, pts.ctypes.data_as(P), len(pts), mode, dist.ctypes.data_as(P),
+                                         value.ctypes.data_as(P),
+                                         proven.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))) == 0
+        pv = proven != 0
+        assert pv.sum() > len(pts) // 2, (mode, int(pv.sum()))  # (most queries are proven by the grid)
+        bad = np.flatnonzero(pv & ((dist != dref) | (value != val)))
+        assert bad.size == 0, (mode, bad[:10], dist[bad[:5]], dref[bad[:5]], value[bad[:5]], val[bad[:5]])
     ch.close()
