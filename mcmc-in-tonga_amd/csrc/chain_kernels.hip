@@ -247,26 +247,6 @@ __device__ __forceinline__ void geo_fill(GridGeo &g, const DevChain &d) {
     g.lb0 = grid_lb_close(lb0);
 }
 
-// One proposal's shared counters and flags.  Shared::pc holds two copies, indexed by the iteration's
-// parity: iteration `it` uses pc[it & 1] from its first barrier-free phase to its last instruction,
-// and wave 0 clears pc[(it + 1) & 1] for the next iteration at the end of `it` -- a copy nothing reads
-// or writes during `it` (its last readers, in iteration it - 1, all passed that iteration's closing
-// barrier).  So no word is cleared while another wave may still read it, whatever the waves' skew.
-// Written in (all of iteration it's copy):
-struct PropCounters {
-    int n_tiles;    // phase B (atomic adds, every tile-pass wave); read in C, F (accounting, tile maxima), G
-    int n_changed;  // phases C, D (mark); read in G
-    int n_orphans;  // phase C (atomic adds); read in D, F (accounting)
-    int n_rays;     // phases C, D (mark); read in E, F, G (and a server's report)
-    int k0;         // phases C, D (mark: atomicMin); read in F, G
-    int accept;     // phase F (tid 0), or a server's next command in G (wave 0, then a block barrier); read in G
-    int pts_seen;   // phase C (atomic adds); read in F (accounting)
-    int ray_pts;    // phase E (atomic adds, rays in HBM); read in F (accounting)
-    int b_done;     // phase B (each tile-pass wave after its release fence); read in C (acquire spin)
-    int e_done;     // phase E (each ray-summing wave after its release fence); read by wave 0 in E (acquire spin)
-    double dsum, dabs;  // phase E (rays in HBM: the terms' changes, any order); read in F
-};
-
 struct Shared {
     GridGeo geo;       // the bucket grid (geo_fill at a launch's start)
     PState ps[2];      // this iteration's proposal (ps[cur]) and the next one guessed in phase F
@@ -277,9 +257,22 @@ struct Shared {
     // estimate in [phi_lo, phi_hi] (held here, not in registers: the kernel is at its VGPR limit)
     int ex_upto;
     double phi_lo, phi_hi, b_lo, b_hi;
-    PropCounters pc[2];  // this proposal's counters, by iteration parity (above)
+    // The proposal's counters (atomic adds in phases B-E; wave 0 clears them at the iteration's end for the
+    // next one).  No wave reads them after phase F's barrier: phase G reads the snapshot gs instead.
+    int n_tiles, n_changed, n_orphans, n_rays, k0;
+    // What phase G needs of the proposal, taken by tid 0 in phase F before its barrier (the counters are
+    // final by then: n_tiles after B, the others after D) and read after it; written again only in the next
+    // iteration's phase F, after the iteration-end barrier -- so nothing writes it while a wave may read it,
+    // and the counters above can be cleared at the iteration's end whatever the waves' skew.  accept: the
+    // decision (phase F), or a server's next command (phase G, wave 0, then a block barrier).
+    struct GSnap {
+        int nc, nr, nt, k0, accept;
+    } gs;
     int ob_lo[3], ob_hi[3], ob_ncand, ob_nfb;  // phase D's orphan-batch search (LDS layout)
     int n_super[2];  // rays in HBM: super-tiles hit, by iteration parity (the next iteration refreshes their maxima)
+    int pts_seen, ray_pts;
+    int e_done;  // LDS layout: waves done with their phase-E rays (waves 1..; wave 0 waits for them)
+    int b_done;  // LDS layout: waves done with their phase-B tile pass (phase B without its barrier)
     // bucket-grid update of an accepted proposal (applied by the last wave in phase G)
     int g_op, g_slot;           // bit 1: remove at old site, bit 2: insert at new site, bit 4: new value in place
     // what the update needs from the grid, read during phase F (G only writes)
@@ -315,8 +308,8 @@ struct Shared {
     DeltaSegs dseg;  // rays in HBM: phase F's new chi^2 partial sums as segments over the old ones
     long long prof[kProfSlots], t_last, t_iter;  // diagnostic phase stamps
     // rays in HBM: the committed terms' sum kept in any order, |tsum - (the exact real sum)| <=
-    // terr; a proposal adds pc.dsum = its terms' changes (any order), pc.dabs = their magnitudes (phase E)
-    double tsum, terr, b_T, b_E;
+    // terr; a proposal adds dsum = its terms' changes (any order), dabs = their magnitudes (phase E)
+    double tsum, terr, dsum, dabs, b_T, b_E;
     double wpart[kChainThreads / 64];  // each wave's part of a block-wide any-order sum of the terms
     // a death, rays in LDS, free-running: phase G's deleteat! shift (shift_range) by waves 1.. -- each
     // wave's last source read in phase F (shift_edge), the waves done counted in shift_done, which wave 0
@@ -800,18 +793,18 @@ __device__ void grid_apply(const DevChain &d, Shared &sh) {
     }
 }
 
-__device__ __forceinline__ void mark(const DevChain &d, const Views &v, Shared &sh, PropCounters &pc, int p, int r,
-                                     int s, double dd, double z) {
+__device__ __forceinline__ void mark(const DevChain &d, const Views &v, Shared &sh, int p, int r, int s, double dd,
+                                     double z) {
     d.cand_s[p] = s;
     d.cand_d[p] = dd;
     d.cand_z[p] = z;
     d.cand_flag[p] = 1;
-    const int c = atomicAdd(&pc.n_changed, 1);
+    const int c = atomicAdd(&sh.n_changed, 1);
     d.changed[c] = p;
     if (c < kChgLds) sh.chg[c] = ChgRec{p, s, dd, z};
     if (atomicExch(&v.rflag[r], 1) == 0) {
-        v.ray_put(atomicAdd(&pc.n_rays, 1), r);
-        atomicMin(&pc.k0, r);
+        v.ray_put(atomicAdd(&sh.n_rays, 1), r);
+        atomicMin(&sh.k0, r);
     }
 }
 
@@ -867,9 +860,9 @@ __device__ __forceinline__ void mb_store(long long *p, long long v) {
 // QUERY commands (one-point Interpolation on the committed model or the model
 // plus one edit -- the state here is the committed one, a pending proposal
 // lives only in the candidate overlay) meanwhile.  EVAL: its steps into
-// sh.srv_*, the pending proposal's fate into `accept`; QUIT or silence:
+// sh.srv_*, the pending proposal's fate into sh.gs.accept; QUIT or silence:
 // sh.srv_quit (and undo).
-__device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shared &sh, int lane, int &accept) {
+__device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shared &sh, int lane) {
     constexpr int kWords = (int)(offsetof(Mailbox, done) / sizeof(long long));
     static_assert(kWords <= 64 && kWords <= (int)(sizeof(sh.mbox) / sizeof(long long)), "mailbox payload");
     long long seen = sh.srv_seq;
@@ -942,10 +935,10 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
                     for (int k = 0; k < ns; ++k) sh.srv_step[k] = c.step[k];
                     sh.srv_n = ns;
                     sh.srv_k = 0;
-                    accept = c.decision != 0 ? 1 : 0;
+                    sh.gs.accept = c.decision != 0 ? 1 : 0;
                     sh.srv_quit = 0;
                 } else {  // quit: the pending proposal (if any) is undone
-                    accept = 0;
+                    sh.gs.accept = 0;
                     sh.srv_quit = 1;
                 }
             }
@@ -954,7 +947,7 @@ __device__ void server_wait(Mailbox *mb, const DevChain &d, const Views &v, Shar
         }
         if ((long long)wall_clock64() - t0 > kServerIdleTicks) {  // no host: undo and return
             if (lane == 0) {
-                accept = 0;
+                sh.gs.accept = 0;
                 sh.srv_quit = 1;
             }
             wave_sync_lds();
@@ -1195,9 +1188,10 @@ __device__ __attribute__((noinline)) double exact_sums(const double *term, doubl
 // A scripted step's answer in the pinned output (wave 0; system-scope stores): [phi, k, (ray, ptS) x k],
 // the changed rays' new t* (the caller holds the model's ptS); k = -1: the whole proposed ptS follows.
 // phi: NaN when the answer goes out before phase F (a server's step: the host forms phi_n itself).
-__device__ void server_report(double *outp, const Views &v, int nr, int n, int lane, double phi) {
+__device__ void server_report(double *outp, const Views &v, const Shared &sh, int n, int lane, double phi) {
     long long *out = reinterpret_cast<long long *>(outp);
     auto put = [&](int i, double x) { mb_store(out + i, __double_as_longlong(x)); };
+    const int nr = sh.n_rays;
     const bool few = 2 * nr + 2 <= n + 1;
     if (few) {
         for (int i = lane; i < nr; i += 64) {
@@ -1353,8 +1347,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         sh.bytes = 0;
         sh.cur = 0;
         sh.defer = 0;
-        for (int k = 0; k < 2; ++k) sh.pc[k] = PropCounters{0, 0, 0, 0, n, 0, 0, 0, 0, 0, 0.0, 0.0};
+        if (!RLDS) sh.dsum = sh.dabs = 0.0;
         sh.grid_fallbacks32 = 0;
+        sh.e_done = sh.b_done = 0;
         geo_fill(sh.geo, d);
         for (int a = 0; a < 5; ++a) sh.proposed[a] = sh.accepted[a] = 0;
         sh.phi = s0.phi;
@@ -1419,7 +1414,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 sh.srv_busy_c = 0;
             }
             wave_sync_lds();
-            server_wait(mb, d, v, sh, lane, sh.pc[0].accept);
+            server_wait(mb, d, v, sh, lane);
         }
         if (rbx) {  // the first round (the last one done is in the slot)
             if (lane == 0) sh.rseq = mb_load(&rbx->slot[bchain].done);
@@ -1436,7 +1431,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 make_proposal(sh.ps[0], P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
                               d.czeta, [&](int pos) { return v.ord[pos]; });
             if (sh.ps[0].p.active) sh.proposed[sh.ps[0].p.action] += 1;
-            sh.pc[0] = PropCounters{0, 0, 0, 0, n, 0, 0, 0, 0, 0, 0.0, 0.0};  // (the first command's decision: none)
+            sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
+            sh.pts_seen = sh.ray_pts = 0;
+            sh.k0 = n;
+            sh.gs.accept = 0;
         }
         if (lane == 0) sh.spec_ok = 0;
     }
@@ -1479,7 +1477,6 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     }
     __syncthreads();
     for (long long it = 0; it < iters && !((mb || rbx || xch) && sh.srv_quit); ++it) {
-        PropCounters &pc = sh.pc[it & 1];  // this proposal's counters (the other copy is the next one's)
         if (prof_on && tid == 0) sh.t_iter = clock64();
         // rays in HBM: the previous accepted proposal's super-tile maxima (their first round of
         // loads issued here, so it overlaps the partial sums' commit below)
@@ -1608,7 +1605,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
 #pragma unroll
                             for (int u = 0; u < 4; ++u)
                                 if (hit[u]) {
-                                    const int k = atomicAdd(&pc.n_tiles, 1);
+                                    const int k = atomicAdd(&sh.n_tiles, 1);
                                     v.thit[k] = rec[u].x;
                                     if (k < v.hrec_cap) v.hrec[k] = rec[u];
                                 }
@@ -1635,7 +1632,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                 const int first = __builtin_ctzll(m), cnt = __popcll(m);
                                 const int rank = __popcll(m & ((1ull << lane) - 1ull));
                                 int base = 0;
-                                if (lane == first) base = atomicAdd(&pc.n_tiles, cnt);  // one atomic per wave
+                                if (lane == first) base = atomicAdd(&sh.n_tiles, cnt);  // one atomic per wave
                                 base = __builtin_amdgcn_readlane(base, first);
                                 if (hit[u]) {
                                     const int t = t0 + u * nthr, slot = npre + rank;
@@ -1682,7 +1679,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
 #pragma unroll
                         for (int u = 0; u < TU; ++u)
                             if (hit[u]) {
-                                const int k = atomicAdd(&pc.n_tiles, 1), t = t0 + u * nthr;
+                                const int k = atomicAdd(&sh.n_tiles, 1), t = t0 + u * nthr;
                                 v.thit[k] = t;
                                 if (!SMALL && k < v.hrec_cap) v.hrec[k] = int4{t, v.tstart[t], v.tray[t], 0};
                             }
@@ -1690,7 +1687,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             }
             if (nobar && !(query && wv == kWv - 1)) {  // (every wave but the query wave: its tile pass is done)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0) atomicAdd(&pc.b_done, 1);
+                if (lane == 0) atomicAdd(&sh.b_done, 1);
                 SKEW(3);
             }
             if (RLDS && action == tdchain::kDeath && nscript) {  // deleteat! shift, staged before we know if it is accepted
@@ -1703,7 +1700,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             }
             if (query && wv == kWv - 1) {  // TD_inversion_function.jl:81 (birth), :146 (death)
                 const bool birth = action == tdchain::kBirth;
-                if (nobar && lane == 0) atomicAdd(&pc.b_done, 1);  // (a death: nothing in phase C waits for this query)
+                if (nobar && lane == 0) atomicAdd(&sh.b_done, 1);  // (a death: nothing in phase C waits for this query)
                 const Nearest r = wave_nearest(d, v, sh, lane, birth ? p.x : kx, birth ? p.y : ky, birth ? p.z : kz,
                                                birth ? -1 : slot_k, -1, 0.0, 0.0, 0.0, 0.0);
                 if (lane == 0) sh.q_zeta = r.z;
@@ -1730,7 +1727,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                                  nobar && action == tdchain::kDeath ? sh.q_zeta : zetanew_death,
                                                  sh.lnN);  // (nobar: this lane asked the death's query itself)
 
-                const int nt = pc.n_tiles;
+                const int nt = sh.n_tiles;
                 // the selected cell's value, known since the proposal was made: czeta[slot_k] = zeta_killed
                 const double zeta_k = slot_k >= 0 ? zeta_killed : 0.0;
                 int seen = 0;
@@ -1739,18 +1736,18 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 auto point = [&](int q, int ray, int s, double bd, double qx, double qy, double qz) {
                     if (action == tdchain::kBirth) {  // appended cell: strict capture
                         const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
-                        if (dd < bd) mark(d, v, sh, pc, q, ray, new_slot, dd, pp.zeta);
+                        if (dd < bd) mark(d, v, sh, q, ray, new_slot, dd, pp.zeta);
                     } else if (action == tdchain::kChange) {
-                        if (s == slot_k) mark(d, v, sh, pc, q, ray, s, bd, pp.zeta);
+                        if (s == slot_k) mark(d, v, sh, q, ray, s, bd, pp.zeta);
                     } else if (s == slot_k) {  // death / move: its points are re-searched
-                        const int o = atomicAdd(&pc.n_orphans, 1);
+                        const int o = atomicAdd(&sh.n_orphans, 1);
                         d.orphans[o] = q;
                         if (o < kOrphanLds) sh.orph[o] = OrphanRec{qx, qy, qz, q, ray};
                     } else if (action == tdchain::kMove) {
                         const double dd = dist2(pp.x, pp.y, pp.z, qx, qy, qz);
                         // (an exact tie: Julia positions, through the stamps -- loaded only then)
                         if (dd < bd || (dd == bd && s >= 0 && d.stamp[slot_k] < d.stamp[s]))
-                            mark(d, v, sh, pc, q, ray, slot_k, dd, zeta_k);
+                            mark(d, v, sh, q, ray, slot_k, dd, zeta_k);
                     }
                 };
                 if constexpr (SMALL) {
@@ -1759,9 +1756,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         point(pre_q, pre_ray, pre_s, pre_bd, pre_x, pre_y, pre_z);
                     }
                     if (nobar)  // the whole hit list from here on: every wave's tile pass done
-                        while (__hip_atomic_load(&pc.b_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kWv)
+                        while (__hip_atomic_load(&sh.b_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kWv)
                             __builtin_amdgcn_s_sleep(1);
-                    const int nt = pc.n_tiles;
+                    const int nt = sh.n_tiles;
                     for (int item = tid; item < nt * kTilePts; item += NTH) {
                         const int t = v.thit[item / kTilePts];
                         if (t < 0) continue;  // preloaded
@@ -1803,13 +1800,13 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                     }
                 }
-                if (seen) atomicAdd(&pc.pts_seen, seen);
+                if (seen) atomicAdd(&sh.pts_seen, seen);
                 __syncthreads();
                 SKEW(5);
                 if (nobar && action == tdchain::kDeath) zetanew_death = sh.q_zeta;  // (the query wave is past it)
                 STAMP(2);
                 // ========= phase D: re-search orphaned points, one wave each =========
-                no = pc.n_orphans;
+                no = sh.n_orphans;
                 const bool death = action == tdchain::kDeath;
                 const int skip_s = death ? slot_k : -1, moved_s = death ? -1 : slot_k;
                 // the orphans the per-wave search takes: all of them in order, or the batch's unproven ones
@@ -1950,7 +1947,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                     if (bs >= 0 && bd < kSentinel && !tie && bd < lb) {
                                         const int q = o < kOrphanLds ? sh.orph[o].q : d.orphans[o];
                                         const int ray = o < kOrphanLds ? sh.orph[o].ray : d.pt_ray[q];
-                                        mark(d, v, sh, pc, q, ray, bs, bd, d.czeta[bs]);
+                                        mark(d, v, sh, q, ray, bs, bd, d.czeta[bs]);
                                     } else {
                                         fb[atomicAdd(&sh.ob_nfb, 1)] = o;
                                     }
@@ -1982,13 +1979,13 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     }
                     const Nearest r =
                         wave_nearest(d, v, sh, lane, qx, qy, qz, skip_s, moved_s, pp.x, pp.y, pp.z, zeta_killed);
-                    if (lane == 0) mark(d, v, sh, pc, q, ray, r.s, r.d, r.z);
+                    if (lane == 0) mark(d, v, sh, q, ray, r.s, r.d, r.z);
                 }
                 if (nlist > 0) __syncthreads();
                 SKEW(10);
                 STAMP(3);
                 // ================= phase E: t* of the rays that changed =================
-                const int nr = pc.n_rays;
+                const int nr = sh.n_rays;
                 const OverlayZeta oz{d.cand_flag, d.cand_z, d.zeta0};
                 // the t* of a changed ray and its chi^2 term (MCsub.jl:147-171), kept beside the old
                 auto ray_done = [&](int r, double val, double tsr, double sgr, double old_term, int npr) {
@@ -1999,13 +1996,13 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     const double nterm = ((df * df) * 1.0) / (sg * sg);  // MCsub.jl:171
                     v.term[r] = nterm;
                     if constexpr (!RLDS) {  // (the running total: any order; rays in LDS re-add them all)
-                        atomicAdd(&pc.dsum, nterm - old_term);
-                        atomicAdd(&pc.dabs, fabs(nterm) + fabs(old_term));
+                        atomicAdd(&sh.dsum, nterm - old_term);
+                        atomicAdd(&sh.dabs, fabs(nterm) + fabs(old_term));
                     }
                     if constexpr (RLDS)  // (the accounting below may run before phase E is over)
                         atomicAdd((unsigned long long *)&sh.bytes, (unsigned long long)npr * 17ull);
                     else
-                        atomicAdd(&pc.ray_pts, npr);
+                        atomicAdd(&sh.ray_pts, npr);
                     if constexpr (WALK)  // an event of the walk (scripted steps: the decisions on bounds need none)
                         if (nscript) atomicOr(&cmask[r >> 6], 1ull << (r & 63));
                 };
@@ -2092,10 +2089,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         // phase F's side work
                         if (wv != 0 && wv < nr) {
                             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                            if (lane == 0) atomicAdd(&pc.e_done, 1);
+                            if (lane == 0) atomicAdd(&sh.e_done, 1);
                         } else if (wv == 0 && nr > 1) {
                             const int want = min(nr, kWv) - 1;
-                            while (__hip_atomic_load(&pc.e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+                            while (__hip_atomic_load(&sh.e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
                                 __builtin_amdgcn_s_sleep(1);
                         }
                         SKEW(11);
@@ -2114,7 +2111,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             // step_cur at the iteration's end, which a wave still in phase G must not see
             const int sdec = nscript ? sh.step_cur.decision : 1;
             if (early && wv == 0) {
-                server_report(sa.out, v, pc.n_rays, n, lane, __builtin_nan(""));
+                server_report(sa.out, v, sh, n, lane, __builtin_nan(""));
                 // the answer's system-scope stores acknowledged before done: no system-scope
                 // fence, which would write back this XCD's L2 at every call
                 __builtin_amdgcn_s_waitcnt(0);
@@ -2140,13 +2137,13 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             // sum is formed afresh from all the terms (block-uniform: every lane reads the same LDS).
             // Rays in LDS: the ~400 terms are re-added every time (one wave, one DPP reduction: as
             // cheap as keeping the total).
-            const double Tp = RLDS ? 0.0 : sh.tsum + pc.dsum;
-            const double Ep = RLDS ? 0.0 : sh.terr + kSumSlack * ((double)(pc.n_rays + 2) * pc.dabs + fabs(Tp));
+            const double Tp = RLDS ? 0.0 : sh.tsum + sh.dsum;
+            const double Ep = RLDS ? 0.0 : sh.terr + kSumSlack * ((double)(sh.n_rays + 2) * sh.dabs + fabs(Tp));
             const bool anchor = RLDS || !(Ep <= 1e-10 * Tp);
             if constexpr (WALK) {
                 // rays in HBM: the whole block adds the proposal's terms afresh in any order --
                 // n / 512 global loads per thread, four in flight
-                if (!nscript && fwd && pc.k0 < n && anchor) {  // (block-uniform)
+                if (!nscript && fwd && sh.k0 < n && anchor) {  // (block-uniform)
                     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
                     int k = tid;
                     for (; k + 3 * NTH < n; k += 4 * NTH) {
@@ -2172,7 +2169,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 }
             }
             if (wv == 0) {
-                const int k0 = pc.k0;
+                const int k0 = sh.k0;
                 if (fwd) {
                     // the terms added in k order (MCsub.jl:170-172), bit for bit, by this
                     // wave (exact_sum.h); phase E put the changed rays' new terms in place
@@ -2270,7 +2267,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                              : tdchain::accept_t(P, inv2t_r, pp, phi_r, phi_n, czeta, zeta_killed,
                                                                  zetanew_death, sh.lnN);
                 acc_r = acc;
-                pc.accept = acc ? 1 : 0;
+                sh.gs = Shared::GSnap{sh.n_changed, sh.n_rays, sh.n_tiles, sh.k0, acc ? 1 : 0};
                 sh.defer = bdec == 2 ? 1 : 0;
                 sh.phi_n = phi_n;
                 if (prof_on) sh.prof[67] += clock64() - tF;  // diagnostic: decision taken
@@ -2302,10 +2299,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                   kz, pp.x, pp.y, pp.z);
                 if (wv == (kWv >= 6 ? kWv - 2 : kWv - 1)) {
                     if (prof_on && lane == 0) {  // diagnostic: work sizes
-                        sh.prof[68] += pc.n_tiles;
-                        sh.prof[69] += pc.pts_seen;
-                        sh.prof[70] += pc.n_changed;
-                        sh.prof[71] += pc.n_rays;
+                        sh.prof[68] += sh.n_tiles;
+                        sh.prof[69] += sh.pts_seen;
+                        sh.prof[70] += sh.n_changed;
+                        sh.prof[71] += sh.n_rays;
                     }
                     if (lane == 0 && fwd) {  // accounting, off wave 0's path
                         atomicAdd((unsigned long long *)&sh.evaluations, 1ull);
@@ -2317,9 +2314,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                   (unsigned long long)((super_on ? (long long)NS * 32 +
                                                                       (long long)sh.n_super[it & 1] * kTilePts * 32
                                                                  : (long long)NT * 32) +
-                                                       (long long)pc.pts_seen * 36 +
+                                                       (long long)sh.pts_seen * 36 +
                                                        (long long)(no + (action <= 2 ? 1 : 0)) * 27 * 8 * 32 +
-                                                       (RLDS ? 0ll : (long long)pc.ray_pts * 17) + (long long)(n - pc.k0) * 28));
+                                                       (RLDS ? 0ll : (long long)sh.ray_pts * 17) + (long long)(n - sh.k0) * 28));
                     }
                     if (lane == 0 && (action == tdchain::kBirth || action == tdchain::kDeath)) {
                         sh.lnN_far[0] = d.logN[max(ncells - 2, 0)];
@@ -2330,7 +2327,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                 // (waves 2..5 of 8, wave 2 of 4) the hit tiles' maxima if the proposal is accepted (a tile =
                 // a DPP row): four items per thread in flight (rays in HBM: ~140 hit tiles, each load a
                 // round trip)
-                const int nt = pc.n_tiles;
+                const int nt = sh.n_tiles;
                 constexpr int MU = 4, MS = (kWv >= 6 ? kWv - 4 : 1) * 64;
                 if constexpr (RLDS) {  // (~8 hit tiles over 4 waves: one item per thread)
                     for (int i = tid - 128; i < nt * kTilePts; i += MS) {
@@ -2380,21 +2377,21 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             STAMP(5);
             SKEW(14);
             // ================= phase G: commit (or undo) =================
-            const int nc = pc.n_changed, nr = pc.n_rays;
-            if (nscript && sdec != 1 && !early && wv == 0) server_report(sa.out, v, pc.n_rays, n, lane, sh.phi_n);
+            const int nc = sh.gs.nc, nr = sh.gs.nr;
+            if (nscript && sdec != 1 && !early && wv == 0) server_report(sa.out, v, sh, n, lane, sh.phi_n);
             if (mb && sdec == kDecideLater) {  // answered before phase F; its fate comes with the next command
-                if (wv == 0) server_wait(mb, d, v, sh, lane, pc.accept);
+                if (wv == 0) server_wait(mb, d, v, sh, lane);
                 __syncthreads();
                 SKEW(15);
-                if (tid == 0) acc_r = pc.accept != 0;
+                if (tid == 0) acc_r = sh.gs.accept != 0;
             }
             // the changed points' global records (two dependent L2 round trips) and the
             // deleteat! shift go to waves 1.., so wave 0 goes straight to its scalars and
             // the next proposal (kW threads, index w = tid - 64)
             constexpr int kW = NTH - 64;
             const int w = tid - 64;
-            if (pc.accept) {
-                const int nt = pc.n_tiles, k0 = pc.k0;
+            if (sh.gs.accept) {
+                const int nt = sh.gs.nt, k0 = sh.gs.k0;
                 if (wv != 0)
                     for (int c = w; c < nc; c += kW) {
                         if (c < kChgLds) {  // (LDS: stores only)
@@ -2496,7 +2493,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         d.cy[sk] = pp.y;
                         d.cz[sk] = pp.z;
                     }
-                    if (!RLDS && !nscript && fwd && pc.k0 < n) {  // the running total follows the committed terms
+                    if (!RLDS && !nscript && fwd && k0 < n) {  // the running total follows the committed terms
                         sh.tsum = sh.b_T;
                         sh.terr = sh.b_E;
                     }
@@ -2504,7 +2501,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         phi_r = sh.phi_n;
                         sh.phi_lo = sh.b_lo;
                         sh.phi_hi = sh.b_hi;
-                    } else if (!(!nscript && fwd && pc.k0 >= n)) {  // (nothing changed: phi_r stays)
+                    } else if (!(!nscript && fwd && k0 >= n)) {  // (nothing changed: phi_r stays)
                         phi_r = sh.phi_n;
                         sh.phi_lo = sh.phi_hi = phi_r;
                         sh.phi = phi_r;
@@ -2607,10 +2604,14 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                     const tdchain::Proposal &np = sh.ps[cur_r].p;
                     if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
                     sh.spec_ok = 0;
-                    // the next iteration's counters: the other parity's copy, which no wave reads or writes in
-                    // this iteration (PropCounters); n_super likewise
-                    sh.pc[(it + 1) & 1] = PropCounters{0, 0, 0, 0, n, 0, 0, 0, 0, 0, 0.0, 0.0};
+                    // the next proposal's counters: no wave reads them after phase F's barrier (phase G reads
+                    // the snapshot sh.gs), so they are clear before the iteration-end barrier whatever the skew
+                    sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
+                    if (!RLDS) sh.dsum = sh.dabs = 0.0;
                     sh.n_super[(it + 1) & 1] = 0;  // the other parity's list is refreshed first
+                    sh.pts_seen = sh.ray_pts = 0;
+                    sh.e_done = sh.b_done = 0;
+                    sh.k0 = n;
                 }
             }
         }

@@ -607,6 +607,8 @@ def test_grid_query_forms_agree(tt, ds, ctx, orc, clustered):
         model = tt.Model(float(len(x)), x, y, z, rng.uniform(1, 49, len(x)))
     else:
         model = tt.random_model(5000, 3)
+        for a, b in ((10, 11), (200, 4000)):  # exact duplicates: a query at the site ties at distance 0
+            model.xCell[b], model.yCell[b], model.zCell[b] = model.xCell[a], model.yCell[a], model.zCell[a]
     prm = tt.define_TDstructrure().replace(max_cells=10000)
     ch = make(tt, ctx, prm, model, 23, tt.TD_ENGINE_DEVICE)
     ch.run(300)
@@ -641,7 +643,8 @@ def test_grid_query_forms_agree(tt, ds, ctx, orc, clustered):
                                          value.ctypes.data_as(P),
                                          proven.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))) == 0
         pv = proven != 0
-        assert pv.sum() > len(pts) // 2, (mode, int(pv.sum()))  # (most queries are proven by the grid)
+        if not clustered:  # (clustered: the packed buckets overflow, and the chain's queries take the full scan)
+            assert pv.sum() > len(pts) // 2, (mode, int(pv.sum()))  # (most queries are proven by the grid)
         bad = np.flatnonzero(pv & ((dist != dref) | (value != val)))
         assert bad.size == 0, (mode, bad[:10], dist[bad[:5]], dref[bad[:5]], value[bad[:5]], val[bad[:5]])
     ch.close()

@@ -9,7 +9,7 @@ T="tests/test_gpu_chain.py tests/test_gpu_bench_parity.py tests/test_gpu_increme
 for nv in "$@"; do
   v=${nv%%=*}; lib=${nv#*=}
   export TD_LIB_PATH=$PWD/$lib
-  timeout -k 10 540 python -u -m pytest $T -q -p no:cacheprovider --timeout 240 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest $T -v -p no:cacheprovider --timeout 150 --timeout-method thread --durations 15 \
     -k "not do_not_hold_back" > $out/$v.log 2>&1
   rc=$?
   echo "$v rc=$rc: $(tail -1 $out/$v.log)"
