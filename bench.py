@@ -20,11 +20,16 @@ Also reported:
                    bound is LATENCY (one persistent workgroup per chain: a
                    chain of dependent barriers and LDS/L2 round trips per
                    proposal); `latency` gives the measured phase cycles.  The
-                   HBM line prices SURVEY 8(d)'s algorithmic bytes of one
-                   evaluate per proposal against HBM peak; `incremental_*`
-                   beside it is what the incremental proposals actually read
-                   (counted in-kernel: tile boxes, candidate points, grid
-                   queries, re-summed ray points, chi^2 terms).
+                   headline's HBM line prices SURVEY 8(d)'s algorithmic bytes
+                   of one evaluate per proposal against HBM peak;
+                   `incremental_*` beside it is what the incremental proposals
+                   actually read (counted in-kernel: tile boxes, candidate
+                   points, grid queries, re-summed ray points, chi^2 terms),
+                   and every other chain block's `frac` is that counted figure
+                   (chain_roofline: no `frac` above 1).
+At N > 1 every multi-rank leg runs under a deadline the ranks agree on
+(run_leg): a stalled collective makes rank 0 print the line it has, with that
+leg as an error, and every rank exit non-zero, instead of hanging.
   full_evaluate -- the drop-in td_evaluate path (brute-force P x N nearest
                    search, MCsub.jl:123-185) on the same model: latency and
                    the FP64-VALU roofline of its dominant kernel.

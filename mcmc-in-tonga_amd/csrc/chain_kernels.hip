@@ -316,6 +316,7 @@ struct Shared {
     // waits for before it reads the order for the next proposal
     int shift_done;
     int shift_edge[kChainThreads / 64];
+    int dbg_site[kChainThreads / 64];  // the skew build's trail: each wave's last skew site (SKEW)
 };
 
 // deleteat! at Julia position `index` (rays in LDS, free-running): positions index+1 .. ncells-1 move down
@@ -348,6 +349,7 @@ __device__ __forceinline__ void shift_range(int index, int ncells, int w, int nw
 #ifdef TD_CHAIN_SKEW
 #define SKEW(site)                                                                      \
     do {                                                                                \
+        if (lane == 0) sh.dbg_site[wv] = (int)((it << 8) | (site));                     \
         if (wv == (int)(((unsigned long long)it * 5ull + (site)) % (unsigned)kWv)) {    \
             __builtin_amdgcn_s_sleep(127);                                              \
             if (((it + (site)) & 1) != 0) __builtin_amdgcn_s_sleep(127);                \
@@ -356,6 +358,34 @@ __device__ __forceinline__ void shift_range(int index, int ncells, int w, int nw
 #else
 #define SKEW(site) \
     do {           \
+    } while (0)
+#endif
+// The chain's spin waits (a wave waiting for other waves' counts in LDS).  In the skew build each gives up
+// after ~0.5 s, adds `site` to the diagnostic slot prof[79] (tdt_chain_profile) and goes on, so a wait that
+// can never end shows up as a wrong answer and a nonzero slot instead of a hung launch.
+#ifdef TD_CHAIN_SKEW
+// (the first time one gives up, prof[56 + w] holds wave w's last skew site, as it << 8 | site, and
+// prof[64] the iteration << 8 | the giving-up wave)
+#define SPIN_WAIT(cond, site)                                                                        \
+    do {                                                                                             \
+        long long n_ = 0;                                                                            \
+        while (cond) {                                                                               \
+            __builtin_amdgcn_s_sleep(1);                                                             \
+            if (++n_ > (1ll << 23)) {                                                                \
+                if (lane == 0) {                                                                     \
+                    if (atomicAdd((unsigned long long *)&sh.prof[79], (unsigned long long)(site)) == 0ull) { \
+                        for (int w_ = 0; w_ < kWv; ++w_) sh.prof[56 + w_] = sh.dbg_site[w_];       \
+                        sh.prof[64] = (it << 8) | wv;                                                \
+                    }                                                                                \
+                }                                                                                    \
+                break;                                                                               \
+            }                                                                                        \
+        }                                                                                            \
+    } while (0)
+#else
+#define SPIN_WAIT(cond, site)                      \
+    do {                                           \
+        while (cond) __builtin_amdgcn_s_sleep(1);  \
     } while (0)
 #endif
 
@@ -1705,12 +1735,20 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                                birth ? -1 : slot_k, -1, 0.0, 0.0, 0.0, 0.0);
                 if (lane == 0) sh.q_zeta = r.z;
             }
-            if (!nobar) {
-                __syncthreads();  // tile list complete, query answered
-                SKEW(4);
-                if (action == tdchain::kBirth) czeta = sh.q_zeta;
-                if (action == tdchain::kDeath) zetanew_death = sh.q_zeta;
-            }
+        }
+        // Phase B's barrier (tile list complete, query answered) -- taken by an inactive proposal too (a birth
+        // at max_cells, a death at min_cells: the reference skips the iteration, nobar stays false).  That one
+        // has no phase B-G, and without this barrier nothing would separate the other waves' reads at the
+        // loop top (sh.cur, the proposal, sh.srv_quit) from wave 0's writes at this iteration's end (the next
+        // proposal goes into ps[cur] when no guess is adopted): a wave still at the loop top would read the
+        // NEXT proposal.  So every iteration has a block barrier between the loop top and wave 0's
+        // end-of-iteration writes (this one, or C's and F's).  Found by the wave-skew build
+        // (tools/skew_probe.py, the 8-cell model at max_cells 12).
+        if (!nobar) {
+            __syncthreads();
+            SKEW(4);
+            if (p.active && action == tdchain::kBirth) czeta = sh.q_zeta;
+            if (p.active && action == tdchain::kDeath) zetanew_death = sh.q_zeta;
         }
         Proposal pp = p;
         if (p.active && action == tdchain::kBirth && !nscript) tdchain::birth_zeta(P, pp, czeta);  // every lane, same value
@@ -1756,8 +1794,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         point(pre_q, pre_ray, pre_s, pre_bd, pre_x, pre_y, pre_z);
                     }
                     if (nobar)  // the whole hit list from here on: every wave's tile pass done
-                        while (__hip_atomic_load(&sh.b_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kWv)
-                            __builtin_amdgcn_s_sleep(1);
+                        SPIN_WAIT(__hip_atomic_load(&sh.b_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kWv, 1);
                     const int nt = sh.n_tiles;
                     for (int item = tid; item < nt * kTilePts; item += NTH) {
                         const int t = v.thit[item / kTilePts];
@@ -2092,8 +2129,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             if (lane == 0) atomicAdd(&sh.e_done, 1);
                         } else if (wv == 0 && nr > 1) {
                             const int want = min(nr, kWv) - 1;
-                            while (__hip_atomic_load(&sh.e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-                                __builtin_amdgcn_s_sleep(1);
+                            SPIN_WAIT(__hip_atomic_load(&sh.e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want,
+                                      1000);
                         }
                         SKEW(11);
                     }
@@ -2587,9 +2624,9 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                         // the shifting waves are done
                         const bool killed = RLDS && acc && action == tdchain::kDeath;
                         if (killed && !nscript)
-                            while (__hip_atomic_load(&sh.shift_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
-                                   kWv - 1)
-                                __builtin_amdgcn_s_sleep(1);
+                            SPIN_WAIT(__hip_atomic_load(&sh.shift_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                                          kWv - 1,
+                                      1000000);
                         auto slot_at = [&](int pos) {
                             return (killed && nscript && pos >= (int)pp.index) ? d.order_tmp[pos + 1] : v.ord[pos];
                         };

@@ -83,9 +83,12 @@ __global__ __launch_bounds__(256) void k_grid_fill(double *__restrict__ cells, c
 // points (rays are ray-major, so neighbouring points are spatial neighbours) and its L2 fetches only the
 // buckets near those, not every bucket of the grid.  A bijection of [0, nblocks): the blocks b = x, x + 8,
 // ... (q + 1 of them for the first nblocks % 8 residues x, else q = nblocks / 8) take consecutive chunks.
+#ifndef TD_NN_XCD
+#define TD_NN_XCD 1  // 0: blocks in dispatch order (A/B builds)
+#endif
 __device__ __forceinline__ int xcd_block(int nblocks) {
     const int b = (int)blockIdx.x, x = b & 7, q = nblocks >> 3, r = nblocks & 7;
-    return x * q + min(x, r) + (b >> 3);
+    return TD_NN_XCD ? x * q + min(x, r) + (b >> 3) : b;
 }
 
 // lexicographic min of (d, i) over each half-wave (32 lanes), to every lane
