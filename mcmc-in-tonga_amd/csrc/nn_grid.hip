@@ -78,19 +78,6 @@ __global__ __launch_bounds__(256) void k_grid_fill(double *__restrict__ cells, c
     if (pos < kGridCap) ent[(long)b * kGridCap + pos] = BucketEntry{x, y, z, i, 0};
 }
 
-// XCD-aware point order: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md, workgroup dispatch), so
-// the blocks of residue b % 8 take consecutive chunks of the point order -- each XCD a contiguous eighth of the
-// points (rays are ray-major, so neighbouring points are spatial neighbours) and its L2 fetches only the
-// buckets near those, not every bucket of the grid.  A bijection of [0, nblocks): the blocks b = x, x + 8,
-// ... (q + 1 of them for the first nblocks % 8 residues x, else q = nblocks / 8) take consecutive chunks.
-#ifndef TD_NN_XCD
-#define TD_NN_XCD 1  // 0: blocks in dispatch order (A/B builds)
-#endif
-__device__ __forceinline__ int xcd_block(int nblocks) {
-    const int b = (int)blockIdx.x, x = b & 7, q = nblocks >> 3, r = nblocks & 7;
-    return TD_NN_XCD ? x * q + min(x, r) + (b >> 3) : b;
-}
-
 // lexicographic min of (d, i) over each half-wave (32 lanes), to every lane
 __device__ __forceinline__ void half_min(double &d, int &i) {
     unsigned long long k = (unsigned long long)__double_as_longlong(d);
@@ -123,9 +110,8 @@ __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, 
                                                  int other_nb) {
     // the other set of bucket counts (the previous search's) is zeroed for the next search
     for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < other_nb; b += gridDim.x * blockDim.x) other_count[b] = 0;
-    const int hl = threadIdx.x & 31;  // lane in the half-wave
-    const int L = xcd_block((int)gridDim.x);
-    const int p = (L * (int)blockDim.x + (int)threadIdx.x) >> 5;  // one point per half-wave
+    const int hl = threadIdx.x & 31;                             // lane in the half-wave
+    const int p = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;  // one point per half-wave
     const int pc = min(p, npts - 1);                              // whole half-waves stay for the DPP
     const double x = qx[pc], y = qy[(long)pc * ys], z = qz[(long)pc * zs];
     const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
@@ -219,8 +205,7 @@ __global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx,
                                                   int other_nb) {
     for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < other_nb; b += gridDim.x * blockDim.x) other_count[b] = 0;
     const int lane = threadIdx.x & 63, sub = threadIdx.x & (kGridLpp - 1);
-    const int L = xcd_block((int)gridDim.x);
-    const int p = (L * (int)blockDim.x + (int)threadIdx.x) / kGridLpp;  // whole quads stay for the DPP
+    const int p = (blockIdx.x * blockDim.x + threadIdx.x) / kGridLpp;  // whole quads stay for the DPP
     const int pc = min(p, npts - 1);
     const double x = qx[pc], y = qy[(long)pc * ys], z = qz[(long)pc * zs];
     const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
