@@ -64,6 +64,11 @@ constexpr int kBatchBuckets = 512;  // buckets in the region at most  // rays in
 // one-wave binade scan with the early-rejection bound is faster there (measured: the walk
 // costs ~1.2k more cycles per proposal at 381 rays x 5000 cells)
 constexpr bool kSmallWalk = false;
+// each iteration's proposal counted at its loop top by wave 1 (1), or when made, by wave 0 at the end of the
+// iteration before (0: one dependent LDS read and atomic more on wave 0's serial path)
+#ifndef TD_COUNT_AT_TOP
+#define TD_COUNT_AT_TOP 1
+#endif
 
 // A changed point's candidate (what mark() stores in the overlay), kept in LDS for the first kChgLds of
 // a proposal: phase G commits them from here with stores only -- no dependent round trips to the
@@ -386,6 +391,19 @@ __device__ __forceinline__ void shift_range(int index, int ncells, int w, int nw
 #define SPIN_WAIT(cond, site)                      \
     do {                                           \
         while (cond) __builtin_amdgcn_s_sleep(1);  \
+    } while (0)
+#endif
+
+// Phase-B probe build (-DTD_B_PROBE, diagnostics only): tid 0's cycles from the phase's start (STAMP(0)) to
+// points inside phase B, summed into prof[72 + k] (those slots' preamble use is off in that build).
+#ifdef TD_B_PROBE
+#define BPROBE(k)                                                       \
+    do {                                                                \
+        if (prof_on && tid == 0) sh.prof[72 + (k)] += clock64() - sh.t_last; \
+    } while (0)
+#else
+#define BPROBE(k) \
+    do {          \
     } while (0)
 #endif
 
@@ -1460,7 +1478,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             else
                 make_proposal(sh.ps[0], P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
                               d.czeta, [&](int pos) { return v.ord[pos]; });
-            if (sh.ps[0].p.active) sh.proposed[sh.ps[0].p.action] += 1;
+            if (!TD_COUNT_AT_TOP && sh.ps[0].p.active) sh.proposed[sh.ps[0].p.action] += 1;
             sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
             sh.pts_seen = sh.ray_pts = 0;
             sh.k0 = n;
@@ -1476,7 +1494,11 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     if (prof_on && tid == 0) {
         const long long t_now = clock64();
         sh.prof[76] += t_now - t_start;  // preamble: mirrors, terms, draws, 1st proposal
+#ifdef TD_B_PROBE
+        if (false) {
+#else
         if (SMALL) {  // its parts (slots of the rays-in-HBM walk diagnostics, unused in this layout)
+#endif
             sh.prof[72] += t_mirror - t_start;
             sh.prof[73] += t_init - t_mirror;
             sh.prof[74] += t_now - t_init;
@@ -1560,6 +1582,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         const int new_slot = cur.new_slot;
         const double zeta_killed = cur.zeta_killed;
         double czeta = 0.0, zetanew_death = 0.0;
+        if (TD_COUNT_AT_TOP && tid == 64 && p.active)  // (off wave 0's path: read in the epilogue only)
+            atomicAdd((unsigned long long *)&sh.proposed[action], 1ull);
         STAMP(0);
         // LDS layout: the points of the first kPre hit tiles a wave finds are loaded in
         // phase B (their global round trip overlaps the B barrier and the birth/death
@@ -1676,6 +1700,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                 }
                             }
                         }
+                        BPROBE(0);  // (tile pass done)
                         if (npre > 0) {
                             if (lane < kTilePts * npre) {
                                 const int g = lane / kTilePts;
@@ -1715,6 +1740,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                     }
             }
+            BPROBE(1);  // (preload issued)
             if (nobar && !(query && wv == kWv - 1)) {  // (every wave but the query wave: its tile pass is done)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == 0) atomicAdd(&sh.b_done, 1);
@@ -1750,6 +1776,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             if (p.active && action == tdchain::kBirth) czeta = sh.q_zeta;
             if (p.active && action == tdchain::kDeath) zetanew_death = sh.q_zeta;
         }
+        BPROBE(2);  // (counted / barrier passed)
         Proposal pp = p;
         if (p.active && action == tdchain::kBirth && !nscript) tdchain::birth_zeta(P, pp, czeta);  // every lane, same value
         STAMP(1);
@@ -2638,8 +2665,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             make_proposal(sh.ps[cur_r], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots,
                                           d.free_slots, d.cx, d.cy, d.cz, d.czeta, slot_at);
                     }
-                    const tdchain::Proposal &np = sh.ps[cur_r].p;
-                    if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
+                    if (!TD_COUNT_AT_TOP) {
+                        const tdchain::Proposal &np = sh.ps[cur_r].p;
+                        if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
+                    }
                     sh.spec_ok = 0;
                     // the next proposal's counters: no wave reads them after phase F's barrier (phase G reads
                     // the snapshot sh.gs), so they are clear before the iteration-end barrier whatever the skew
