@@ -27,9 +27,6 @@ Also reported:
                    points, grid queries, re-summed ray points, chi^2 terms),
                    and every other chain block's `frac` is that counted figure
                    (chain_roofline: no `frac` above 1).
-At N > 1 every multi-rank leg runs under a deadline the ranks agree on
-(run_leg): a stalled collective makes rank 0 print the line it has, with that
-leg as an error, and every rank exit non-zero, instead of hanging.
   full_evaluate -- the drop-in td_evaluate path (brute-force P x N nearest
                    search, MCsub.jl:123-185) on the same model: latency and
                    the FP64-VALU roofline of its dominant kernel.
@@ -40,7 +37,9 @@ leg as an error, and every rank exit non-zero, instead of hanging.
 At N > 1 ranks every rank also runs BASELINE config 4 (`config4_ranks`: one
 tempered replica per rank, a swap round every 10 proposals through the
 allgather -- RCCL over xGMI) and config 5 (`stress_chains`: one 10k x 20k
-stress chain per rank).
+stress chain per rank).  Each multi-rank leg runs under a deadline the ranks
+agree on (run_leg): a stalled collective makes rank 0 print the line it has,
+with that leg as an error, and every rank exit non-zero, instead of hanging.
 """
 import argparse
 import json
@@ -259,43 +258,49 @@ def launch_check(world, rank, deadline_s):
 def run_leg(name, fn, dist, coll_dev, rank, out, deadline_s, later):
     """One multi-rank leg of an N > 1 run under a deadline the ranks agree on:
     rank 0's wall clock + deadline_s, taken as the MAX over the ranks (one host,
-    one clock).  A leg that stalls -- a collective some rank never joins (the
-    first multi-rank RCCL traffic over xGMI happens here) -- cannot be left
-    inside its process: a watchdog thread then has rank 0 print the JSON line
-    with everything measured so far (the headline first), this leg as
+    one clock; until they have agreed, each rank's own clock + deadline_s).  A
+    leg that stalls -- a collective some rank never joins (the first
+    multi-rank RCCL traffic over xGMI happens here) -- cannot be left inside
+    its process: a watchdog thread then has rank 0 print the JSON line with
+    everything measured so far (the headline first), this leg as
     {"error": "deadline"} and the `later` legs as skipped, and every rank exit
-    with status 3.  Testing: TD_BENCH_STALL_LEG="name:rank" stalls that rank
-    in that leg before its first collective."""
+    with status 3.  A leg that raises is reported as {"error": ...} and the
+    run goes on.  Testing: TD_BENCH_STALL_LEG="name:rank" stalls that rank in
+    that leg before its first collective."""
     import threading
 
     import torch
 
-    t = torch.tensor([time.time() + deadline_s], dtype=torch.float64, device=coll_dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    until = float(t.item())
+    state = {"until": time.time() + deadline_s}
     done = threading.Event()
 
     def expire():
-        if done.wait(max(0.0, until - time.time())):
-            return
-        if rank == 0:
-            o = dict(out)
-            o[name] = {"error": "deadline", "deadline_s": deadline_s,
-                       "note": "a rank did not finish this leg in time (stalled collective?); the process exits"}
-            for k in later:
-                o[k] = {"error": "skipped: an earlier multi-rank leg passed its deadline"}
-            sys.stdout.write(json.dumps(o) + "\n")
-            sys.stdout.flush()
-        sys.stderr.write("bench.py rank %d: leg %s passed its deadline (%.0f s); exiting\n" % (rank, name, deadline_s))
-        sys.stderr.flush()
-        os._exit(3)
+        while not done.wait(0.25):
+            if time.time() < state["until"]:
+                continue
+            if rank == 0:
+                o = dict(out)
+                o[name] = {"error": "deadline", "deadline_s": deadline_s,
+                           "note": "a rank did not finish this leg in time (stalled collective?); the process exits"}
+                for k in later:
+                    o[k] = {"error": "skipped: an earlier multi-rank leg passed its deadline"}
+                sys.stdout.write(json.dumps(o) + "\n")
+                sys.stdout.flush()
+            sys.stderr.write("bench.py rank %d: leg %s passed its deadline (%.0f s); exiting\n" % (rank, name, deadline_s))
+            sys.stderr.flush()
+            os._exit(3)
 
     threading.Thread(target=expire, name="leg-deadline-" + name, daemon=True).start()
     try:
+        t = torch.tensor([state["until"]], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        state["until"] = float(t.item())
         if os.environ.get("TD_BENCH_STALL_LEG") == "%s:%d" % (name, rank):
             while True:
                 time.sleep(1.0)
         return fn()
+    except Exception as e:  # (a leg that fails on this rank; a rank left waiting for it hits the deadline)
+        return {"error": repr(e)[:300]}
     finally:
         done.set()
 
