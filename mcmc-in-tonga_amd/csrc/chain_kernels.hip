@@ -64,11 +64,6 @@ constexpr int kBatchBuckets = 512;  // buckets in the region at most  // rays in
 // one-wave binade scan with the early-rejection bound is faster there (measured: the walk
 // costs ~1.2k more cycles per proposal at 381 rays x 5000 cells)
 constexpr bool kSmallWalk = false;
-// each iteration's proposal counted at its loop top by wave 1 (1), or when made, by wave 0 at the end of the
-// iteration before (0: one dependent LDS read and atomic more on wave 0's serial path)
-#ifndef TD_COUNT_AT_TOP
-#define TD_COUNT_AT_TOP 1
-#endif
 
 // A changed point's candidate (what mark() stores in the overlay), kept in LDS for the first kChgLds of
 // a proposal: phase G commits them from here with stores only -- no dependent round trips to the
@@ -890,6 +885,42 @@ __device__ __forceinline__ bool tile_may_hit(const float *lo, const float *hi, i
     return s * (1.0f - 0x1p-20f) <= thr;
 }
 __device__ __forceinline__ float tile_thr(double mx) { return (float)mx * (1.0f + 0x1p-20f); }
+
+// The same filter in about half the VALU operations (phase B's tile pass, LDS layout; TD_TILE2): the
+// query's rounding folded into two per-query bounds per axis, one max3 per axis, the squares summed with
+// FMAs.  Never says "no" for a tile holding a point p with dist2(q, p) <= mx (FP64), thr = tile_thr(mx):
+// with E = max_a |(float)q_a| 2^-23 >= |q_a - (float)q_a| on every axis, up = fl((float)q + 2E) >= q and
+// dn = fl((float)q - 2E) <= q (the rounding of the add is at most E/2); for p in the outward-rounded box,
+// |p_a - q_a| >= max(lo - up, dn - hi, 0) >= g_a (1 - 2^-24) with g_a the rounded max3; the FMA sum s
+// errs by at most 3 ulps, so the real sum of the squared gaps -- a lower bound of the exact squared
+// distance, itself within 2^-50 of the FP64 one -- is >= s (1 - 2^-21); and thr >= mx (1 - 2^-24)^2
+// (1 + 2^-20), so s > thr implies dist2(q, p) > mx for every point of the tile.
+#ifndef TD_TILE2
+#define TD_TILE2 1
+#endif
+struct TileQuery2 {
+    float ux, uy, uz, dx, dy, dz;  // the query's upper and lower bounds per axis
+};
+__device__ __forceinline__ TileQuery2 tile_query2(double x, double y, double z) {
+    const float fx = (float)x, fy = (float)y, fz = (float)z;
+    const float e2 = fmaxf(fmaxf(fabsf(fx), fabsf(fy)), fabsf(fz)) * 0x1p-22f;  // 2E
+    return TileQuery2{fx + e2, fy + e2, fz + e2, fx - e2, fy - e2, fz - e2};
+}
+struct TileBox {
+    float lx, ly, lz, hx, hy, hz, thr;
+};
+__device__ __forceinline__ TileBox tile_box(const float *lo, const float *hi, const double *maxd, int nt, int t) {
+    return TileBox{lo[t], lo[nt + t], lo[2 * nt + t], hi[t], hi[nt + t], hi[2 * nt + t], tile_thr(maxd[t])};
+}
+__device__ __forceinline__ bool tile_may_hit2(const TileBox &b, const TileQuery2 &q) {
+    const float gx = fmaxf(fmaxf(b.lx - q.ux, q.dx - b.hx), 0.0f);
+    const float gy = fmaxf(fmaxf(b.ly - q.uy, q.dy - b.hy), 0.0f);
+    const float gz = fmaxf(fmaxf(b.lz - q.uz, q.dz - b.hz), 0.0f);
+    float s = gx * gx;
+    s = __builtin_fmaf(gy, gy, s);
+    s = __builtin_fmaf(gz, gz, s);
+    return s <= b.thr;
+}
 // x rounded up to FP32 (x >= 0; the super-tile maxima)
 __device__ __forceinline__ float f32_up(double x) {
     const float f = (float)x;
@@ -1478,7 +1509,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             else
                 make_proposal(sh.ps[0], P, draws[0], sh.ncells, sh.nfree, sh.nslots, d.free_slots, d.cx, d.cy, d.cz,
                               d.czeta, [&](int pos) { return v.ord[pos]; });
-            if (!TD_COUNT_AT_TOP && sh.ps[0].p.active) sh.proposed[sh.ps[0].p.action] += 1;
+            if (sh.ps[0].p.active) sh.proposed[sh.ps[0].p.action] += 1;
             sh.n_tiles = sh.n_changed = sh.n_orphans = sh.n_rays = 0;
             sh.pts_seen = sh.ray_pts = 0;
             sh.k0 = n;
@@ -1582,8 +1613,6 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
         const int new_slot = cur.new_slot;
         const double zeta_killed = cur.zeta_killed;
         double czeta = 0.0, zetanew_death = 0.0;
-        if (TD_COUNT_AT_TOP && tid == 64 && p.active)  // (off wave 0's path: read in the epilogue only)
-            atomicAdd((unsigned long long *)&sh.proposed[action], 1ull);
         STAMP(0);
         // LDS layout: the points of the first kPre hit tiles a wave finds are loaded in
         // phase B (their global round trip overlaps the B barrier and the birth/death
@@ -1665,19 +1694,43 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                                 }
                         }
                 } else if (SMALL) {
+                    const TileQuery2 tr0 = tile_query2(kx, ky, kz), tr1 = tile_query2(p.x, p.y, p.z);
                     if (tid < nthr) {  // wave-uniform
                         int npre = 0;  // preload slots this wave has taken (wave-uniform)
                         int pt[kPre] = {0, 0, 0, 0};  // their tiles (wave-uniform: from the ballots, no LDS)
                         for (int b0 = wv * 64; b0 < NT; b0 += TU * nthr) {  // the same trip count in every lane
                             const int t0 = b0 + lane;
                             bool hit[TU];
+                            if constexpr (TD_TILE2) {
+                                // every box loaded first (one round of LDS loads), then only the sites the action
+                                // has, on scalar branches (the action made wave-uniform for the compiler)
+                                TileBox bx[TU];
 #pragma unroll
-                            for (int u = 0; u < TU; ++u) {
-                                const int t = min(t0 + u * nthr, NT - 1);  // clamped: loads stay unconditional
-                                const float thr = tile_thr(v.tmaxd[t]);
-                                const bool h0 = tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr);
-                                const bool h1 = tile_may_hit(v.tlo, v.thi, NT, t, tq1, thr);
-                                hit[u] = t0 + u * nthr < NT && ((q0 && h0) || (q1 && h1));
+                                for (int u = 0; u < TU; ++u)
+                                    bx[u] = tile_box(v.tlo, v.thi, v.tmaxd, NT, min(t0 + u * nthr, NT - 1));
+                                const int au = __builtin_amdgcn_readfirstlane(action);
+                                const bool s0 = au != tdchain::kBirth, s1 = au == tdchain::kBirth || au == tdchain::kMove;
+#pragma unroll
+                                for (int u = 0; u < TU; ++u) hit[u] = false;
+                                if (s0) {
+#pragma unroll
+                                    for (int u = 0; u < TU; ++u) hit[u] = tile_may_hit2(bx[u], tr0);
+                                }
+                                if (s1) {
+#pragma unroll
+                                    for (int u = 0; u < TU; ++u) hit[u] = hit[u] || tile_may_hit2(bx[u], tr1);
+                                }
+#pragma unroll
+                                for (int u = 0; u < TU; ++u) hit[u] = hit[u] && t0 + u * nthr < NT;
+                            } else {
+#pragma unroll
+                                for (int u = 0; u < TU; ++u) {
+                                    const int t = min(t0 + u * nthr, NT - 1);  // clamped: loads stay unconditional
+                                    const float thr = tile_thr(v.tmaxd[t]);
+                                    const bool h0 = tile_may_hit(v.tlo, v.thi, NT, t, tq0, thr);
+                                    const bool h1 = tile_may_hit(v.tlo, v.thi, NT, t, tq1, thr);
+                                    hit[u] = t0 + u * nthr < NT && ((q0 && h0) || (q1 && h1));
+                                }
                             }
 #pragma unroll
                             for (int u = 0; u < TU; ++u) {
@@ -2665,10 +2718,8 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             make_proposal(sh.ps[cur_r], P, draws[(it + 1) & 63], sh.ncells, sh.nfree, sh.nslots,
                                           d.free_slots, d.cx, d.cy, d.cz, d.czeta, slot_at);
                     }
-                    if (!TD_COUNT_AT_TOP) {
-                        const tdchain::Proposal &np = sh.ps[cur_r].p;
-                        if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
-                    }
+                    const tdchain::Proposal &np = sh.ps[cur_r].p;
+                    if (np.active) atomicAdd((unsigned long long *)&sh.proposed[np.action], 1ull);
                     sh.spec_ok = 0;
                     // the next proposal's counters: no wave reads them after phase F's barrier (phase G reads
                     // the snapshot sh.gs), so they are clear before the iteration-end barrier whatever the skew
