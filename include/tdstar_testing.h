@@ -49,6 +49,11 @@ int tdt_chain_query_lat(td_chain *ch, const double *pts, int nq, int mode, int64
 /* Each query's answer from the chain's grid search (mode 0: the LDS grid copy with the global first
  * bound; 6: the descriptor-reading form): squared distance, the winning cell's value, proven (1) or
  * left to the full scan (0). */
+/* The chain's phase-B tile filter on caller boxes (FP32, SoA: x of every tile, then y, then z), FP64 tile
+ * maxima and FP64 queries (x, y, z each): hit[q * nt + t] = 1 if tile t passes for query q.  mode 0: the
+ * filter of the HBM layout's super-tiles; 1: the LDS layout's tile pass (tile_may_hit2). */
+int tdt_tile_filter(const float *lo, const float *hi, const double *maxd, int nt, const double *queries, int nq,
+                    int mode, uint8_t *hit);
 int tdt_chain_query_answers(td_chain *ch, const double *pts, int nq, int mode, double *dist, double *value,
                             int32_t *proven);
 /* Metropolis-Hastings decision, eqs. 14-17 (:96-97, :151-152, :196, :241). */

@@ -96,6 +96,9 @@ SIGNATURES = {
     "tdt_chain_lds": (ctypes.c_int, [_vp, _pi64]),
     "tdt_chain_query_lat": (ctypes.c_int, [_vp, _pd, ctypes.c_int, ctypes.c_int, _pi64]),
     "tdt_chain_query_answers": (ctypes.c_int, [_vp, _pd, ctypes.c_int, ctypes.c_int, _pd, _pd, _pi32]),
+    "tdt_tile_filter": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), _pd,
+                                       ctypes.c_int, _pd, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_uint8)]),
     "tdt_set_nn_method": (ctypes.c_int, [_vp, ctypes.c_int]),
     "tdt_nn_bench": (ctypes.c_int, [_vp, _pd, _pd, _pd, _pd, _i64, ctypes.c_int, ctypes.c_int, _pd]),
     "tdt_chain_set_lds_mode": (ctypes.c_int, [_vp, ctypes.c_int]),

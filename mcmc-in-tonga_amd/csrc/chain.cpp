@@ -1856,6 +1856,31 @@ int tdt_chain_query_lat(td_chain *ch, const double *pts, int nq, int mode, int64
     return TD_OK;
 }
 
+int tdt_tile_filter(const float *lo, const float *hi, const double *maxd, int nt, const double *queries, int nq,
+                    int mode, uint8_t *hit) {
+    if (!lo || !hi || !maxd || !queries || !hit || nt < 1 || nq < 1 || (mode != 0 && mode != 1)) return TD_ERR_ARG;
+    float *dlo = nullptr, *dhi = nullptr;
+    double *dm = nullptr, *dq = nullptr;
+    unsigned char *dh = nullptr;
+    const size_t T = (size_t)nt, Q = (size_t)nq;
+    hipError_t e = hipMalloc((void **)&dlo, sizeof(float) * 3 * T);
+    if (e == hipSuccess) e = hipMalloc((void **)&dhi, sizeof(float) * 3 * T);
+    if (e == hipSuccess) e = hipMalloc((void **)&dm, sizeof(double) * T);
+    if (e == hipSuccess) e = hipMalloc((void **)&dq, sizeof(double) * 3 * Q);
+    if (e == hipSuccess) e = hipMalloc((void **)&dh, T * Q);
+    if (e == hipSuccess) e = hipMemcpy(dlo, lo, sizeof(float) * 3 * T, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dhi, hi, sizeof(float) * 3 * T, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dm, maxd, sizeof(double) * T, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dq, queries, sizeof(double) * 3 * Q, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = test_tile_filter(dlo, dhi, dm, nt, dq, nq, mode, dh, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(hit, dh, T * Q, hipMemcpyDeviceToHost);
+    for (void *p : {(void *)dlo, (void *)dhi, (void *)dm, (void *)dq, (void *)dh})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return set_err(nullptr, TD_ERR_HIP, std::string("tdt_tile_filter: ") + hipGetErrorString(e));
+    return TD_OK;
+}
+
 int tdt_chain_query_answers(td_chain *ch, const double *pts, int nq, int mode, double *dist, double *value,
                             int32_t *proven) {
     if (!ch || ch->engine != TD_ENGINE_DEVICE || !pts || nq < 1 || !dist || !value || !proven ||

@@ -312,6 +312,8 @@ int shadow_chain_query(td_chain *ch, double x, double y, double z, const ScriptS
 // Testing: cycles of nq back-to-back grid queries by one wave (k_test_query_lat; mode 0 whole, 1 loads, 2 math)
 hipError_t test_query_lat(const DevChain *dev, const double *pts, int nq, int mode, long long *out, hipStream_t s);
 // Testing: each query's (squared distance, value, proven) from the chain's grid search (k_test_query_answers)
+hipError_t test_tile_filter(const float *lo, const float *hi, const double *maxd, int nt, const double *qs, int nq,
+                            int mode, unsigned char *out, hipStream_t s);
 hipError_t test_query_answers(const DevChain *dev, const double *pts, int nq, int mode, double *out_d, double *out_z,
                               int *out_p, hipStream_t s);
 // LDS bytes of the two layouts, whether super-tiles fit, and the layout chain_run takes.

@@ -3052,6 +3052,33 @@ __global__ __launch_bounds__(64) void k_test_query_answers(const DevChain *__res
     }
 }
 
+// Testing: the phase-B tile filter on given FP32 boxes (SoA, 3 x nt each), FP64 tile maxima and FP64
+// queries: out[q * nt + t] = 1 if the filter lets tile t through for query q (mode 0 tile_may_hit, 1
+// tile_may_hit2).  The tests hold it to "never drops a tile holding a point within the maximum".
+__global__ void k_test_tile_filter(const float *__restrict__ lo, const float *__restrict__ hi,
+                                   const double *__restrict__ maxd, int nt, const double *__restrict__ qs, int nq,
+                                   int mode, unsigned char *__restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)nt * nq) return;
+    const int t = (int)(i % nt), q = (int)(i / nt);
+    const double x = qs[3 * q], y = qs[3 * q + 1], z = qs[3 * q + 2];
+    bool h;
+    if (mode == 0) {
+        h = tile_may_hit(lo, hi, nt, t, tile_query(x, y, z), tile_thr(maxd[t]));
+    } else {
+        h = tile_may_hit2(tile_box(lo, hi, maxd, nt, t), tile_query2(x, y, z));
+    }
+    out[i] = h ? 1 : 0;
+}
+
+hipError_t test_tile_filter(const float *lo, const float *hi, const double *maxd, int nt, const double *qs, int nq,
+                            int mode, unsigned char *out, hipStream_t s) {
+    const long long n = (long long)nt * nq;
+    hipLaunchKernelGGL(k_test_tile_filter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lo, hi, maxd, nt, qs,
+                       nq, mode, out);
+    return hipGetLastError();
+}
+
 hipError_t test_query_answers(const DevChain *dev, const double *pts, int nq, int mode, double *out_d, double *out_z,
                               int *out_p, hipStream_t s) {
     hipLaunchKernelGGL(k_test_query_answers, dim3(1), dim3(64), 0, s, dev, pts, nq, mode, out_d, out_z, out_p);
