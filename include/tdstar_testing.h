@@ -103,27 +103,6 @@ int tdt_rounds_force_exit(td_rounds *r, const int32_t *slots, int64_t nslots);
  * [15] chi^2 and copy-out; [16] the resident server's busy time by its own
  * clock (command seen -> answered), evaluate commands, [17] queries. */
 int tdt_dropin_timing(td_ctx *ctx, int reset, int64_t out[18]);
-/* td_evaluate's full path as one resident launch (eval_server.h; replaces the
- * fill / search / ray-sum launches of MCsub.jl:123-185's evaluate, same
- * answer).  mode 1 (default): grid-path evaluates go through it when no other
- * resident launch of the thread runs; 2: the same with per-workgroup phase
- * stamps (diagnostics); 0: always the launches.  idle_us / guard_us > 0
- * override its idle watchdog (20 ms) and its grid-barrier guard (100 ms) --
- * testing.  Stops a running one. */
-int tdt_eval_server_config(td_ctx *ctx, int mode, int64_t idle_us, int64_t guard_us);
-/* Its counters: [0] evaluates served, [1] launches, [2] failed launches, [3]
- * device time of the served evaluates by the kernel's clock, ns (command taken
- * by workgroup 0 -> last shard finished), [4] running, [5] off for this
- * context, [6] workgroups, [7] points of the largest workgroup share; mode 2:
- * [8..17] summed ns from workgroup 0's take to the last workgroup's stamp j
- * (eval_server.h EvalStamps), [18] evaluates stamped; [19] 0. */
-int tdt_eval_server_stats(td_ctx *ctx, int64_t out[20]);
-/* Diagnostics (mode 2): wave 0's first search round, summed over workgroups
- * and stamped evaluates: [0] ns from the grid barrier to its first loads back,
- * [1] ns to its quads reduced, [2] points its 3x3x3 blocks did not prove, [3]
- * the most entries in one of its buckets, [4] ns for the unproven points, [5]
- * ns for the zeta lookup and the rest of the round. */
-int tdt_eval_server_search_diag(td_ctx *ctx, int64_t out[6]);
 /* The block-wide exact sequential sum (exact_sum.h, used for chi^2 over long
  * ray lists): prefix[k] = C0 + term[0] + ... + term[k] added strictly left to
  * right in FP64 (MCsub.jl:170-172).  *fast = 1 when the parallel path proved

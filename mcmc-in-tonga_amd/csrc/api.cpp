@@ -132,20 +132,14 @@ int ensure_cells(td_ctx *ctx, int64_t ncells) {
     if (ncells <= ctx->cell_cap && ctx->cells) return TD_OK;
     int64_t cap = ctx->cell_cap > 0 ? ctx->cell_cap : 256;
     while (cap < ncells) cap *= 2;
-    (void)eval_server_stop(ctx);  // (hipFree waits for the device: a resident launch would hold it until its watchdog)
     if (ctx->cells) (void)hipFree(ctx->cells);
     if (ctx->h_cells) (void)hipHostFree(ctx->h_cells);
     ctx->cells = nullptr;
     ctx->h_cells = nullptr;
     ctx->cell_cap = 0;
     TD_HIP(ctx, hipMalloc(&ctx->cells, sizeof(double) * 4 * (size_t)cap));
-    // coherent (fine-grained): the resident full evaluate reads it while it stays resident
-    static const bool nc = [] {  // (A/B: TD_STAGE_NC=1)
-        const char *v = std::getenv("TD_STAGE_NC");
-        return v && std::atoi(v) == 1;
-    }();
     TD_HIP(ctx, hipHostMalloc(&ctx->h_cells, sizeof(double) * 4 * (size_t)cap,
-                              hipHostMallocMapped | (nc ? hipHostMallocNonCoherent : hipHostMallocCoherent)));
+                              hipHostMallocMapped | hipHostMallocNonCoherent));
     TD_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->h_cells_dev), ctx->h_cells, 0));
     ctx->cell_cap = cap;
     return TD_OK;
@@ -272,28 +266,6 @@ int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z
     const int64_t t1 = now_ns();
     const auto &g = ctx->g;
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
-    // The grid path through the resident launch (eval_server.cpp) when nothing else of this thread is
-    // resident; per-kernel timing and the nearest indices take the launches.
-    if (ctx->cells_stage && !nearest_out && !tm && g.P > 0 && !resident_others(ctx)) {
-        const CellGrid G = make_cell_grid(ctx->cell_lo, ctx->cell_hi, (double)ncells / 2.0, 4096, kGridMaxBuckets);
-        bool served = false;
-        int64_t issue = 0;
-        rc = eval_server_run(ctx, ncells, G, &served, &issue);
-        if (rc) return rc;
-        if (served) {
-            ctx->cells_stage = nullptr;  // the server's fill made the device copy
-            const int64_t t3 = now_ns();
-            const double phi = host_chi2(ctx->h_out + 1, ctx->tS_host.data(), ctx->sig_host.data(), g.n);
-            if (phi_out) *phi_out = phi;
-            if (ptS_out && g.n) std::memcpy(ptS_out, ctx->h_out + 1, sizeof(double) * (size_t)g.n);
-            const int64_t t4 = now_ns();
-            ctx->dropin_ns[12] += t1 - t0;
-            ctx->dropin_ns[13] += issue;
-            ctx->dropin_ns[14] += t3 - t1 - issue;
-            ctx->dropin_ns[15] += t4 - t3;
-            return TD_OK;
-        }
-    }
     hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, ncells, ctx->best_i, ctx->best_d, ctx->zeta0);
     if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
     // ptS lands in pinned host memory straight from the kernel (no copy back)
@@ -326,7 +298,6 @@ namespace {
 
 void free_ctx(td_ctx *c) {
     if (!c) return;
-    eval_server_free(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     shadow_free(c);
     c->timer.release();
@@ -571,10 +542,7 @@ int td_evaluate(td_ctx *ctx, const double *xCell, const double *yCell, const dou
     if (nCells > 0x7fffffff) return set_err(ctx, TD_ERR_ARG, "td_evaluate: too many cells");
     const int64_t t0 = now_ns();
     TD_HIP(ctx, hipSetDevice(ctx->device));
-    if (nearest_out || !ctx->incremental)
-        servers_quiesce(nullptr, ctx);  // (the full path keeps this context's resident full evaluate)
-    else
-        servers_quiesce(shadow_chain_of(ctx));
+    servers_quiesce((nearest_out || !ctx->incremental) ? nullptr : shadow_chain_of(ctx));
     int rc = (nearest_out || !ctx->incremental)
                  ? evaluate_full(ctx, xCell, yCell, zCell, zeta, nCells, ptS_out, phi_out, nearest_out)
                  : evaluate_incremental(ctx, xCell, yCell, zCell, zeta, nCells, ptS_out, phi_out);
@@ -596,7 +564,7 @@ int td_evaluate_batch(td_ctx *ctx, int64_t nmodels, const int64_t *cell_off, con
         if (b > a && (!xCell || !yCell || !zCell || !zeta))
             return set_err(ctx, TD_ERR_ARG, "td_evaluate_batch: bad cell arrays");
         TD_HIP(ctx, hipSetDevice(ctx->device));
-        servers_quiesce(nullptr, ctx);
+        servers_quiesce(nullptr);
         // independent models: the full evaluate (no shadow chain)
         int rc = evaluate_full(ctx, xCell + a, yCell + a, zCell + a, zeta + a, b - a,
                                ptS_out ? ptS_out + k * ctx->g.n : nullptr, phi_out ? phi_out + k : nullptr);

@@ -560,8 +560,7 @@ int server_stop(td_chain *ch);
 // thread (a Python finaliser may run anywhere) leaves no entry behind.
 struct Resident {
     td_chain *srv;    // a td_evaluate shadow server, or
-    td_rounds *rnd;   // a resident tempering launch, or
-    td_ctx *ev;       // a context's resident full evaluate (eval_server.cpp)
+    td_rounds *rnd;   // a resident tempering launch
     std::thread::id owner;
 };
 std::mutex g_res_mu;
@@ -570,7 +569,7 @@ int rounds_stop(td_rounds *r);
 
 void servers_register(td_chain *ch) {
     std::lock_guard<std::mutex> g(g_res_mu);
-    g_res.push_back(Resident{ch, nullptr, nullptr, std::this_thread::get_id()});
+    g_res.push_back(Resident{ch, nullptr, std::this_thread::get_id()});
 }
 void servers_unregister(td_chain *ch) {
     std::lock_guard<std::mutex> g(g_res_mu);
@@ -579,7 +578,7 @@ void servers_unregister(td_chain *ch) {
 }
 void rounds_register(td_rounds *r) {
     std::lock_guard<std::mutex> g(g_res_mu);
-    g_res.push_back(Resident{nullptr, r, nullptr, std::this_thread::get_id()});
+    g_res.push_back(Resident{nullptr, r, std::this_thread::get_id()});
 }
 void rounds_unregister(td_rounds *r) {
     std::lock_guard<std::mutex> g(g_res_mu);
@@ -590,7 +589,7 @@ void rounds_unregister(td_rounds *r) {
 }  // namespace
 
 namespace tdstar {
-void servers_quiesce(const td_chain *keep, const td_ctx *keep_eval) {
+void servers_quiesce(const td_chain *keep) {
     std::vector<Resident> mine;
     {
         std::lock_guard<std::mutex> g(g_res_mu);
@@ -600,23 +599,7 @@ void servers_quiesce(const td_chain *keep, const td_ctx *keep_eval) {
     for (const Resident &e : mine) {
         if (e.srv && e.srv != keep) (void)server_stop(e.srv);
         if (e.rnd) (void)rounds_stop(e.rnd);
-        if (e.ev && e.ev != keep_eval) (void)eval_server_stop(e.ev);
     }
-}
-void resident_register_eval(td_ctx *ctx) {
-    std::lock_guard<std::mutex> g(g_res_mu);
-    g_res.push_back(Resident{nullptr, nullptr, ctx, std::this_thread::get_id()});
-}
-void resident_unregister_eval(td_ctx *ctx) {
-    std::lock_guard<std::mutex> g(g_res_mu);
-    g_res.erase(std::remove_if(g_res.begin(), g_res.end(), [&](const Resident &e) { return e.ev == ctx; }),
-                g_res.end());
-}
-bool resident_others(const td_ctx *ctx) {
-    std::lock_guard<std::mutex> g(g_res_mu);
-    for (const Resident &e : g_res)
-        if (e.owner == std::this_thread::get_id() && e.ev != ctx) return true;
-    return false;
 }
 }  // namespace tdstar
 
@@ -1357,8 +1340,7 @@ int td_chain_run(td_chain *ch, int64_t iterations) {
     if (iterations == 0) return TD_OK;
     hipError_t e = hipSetDevice(ch->ctx->device);
     if (e != hipSuccess) return hip_err(ch->ctx, e, "hipSetDevice");
-    // DROPIN's td_evaluate keeps its own server; HOST's full evaluates keep the context's resident one
-    if (ch->engine != TD_ENGINE_DROPIN) servers_quiesce(nullptr, ch->engine == TD_ENGINE_HOST ? ch->ctx : nullptr);
+    if (ch->engine != TD_ENGINE_DROPIN) servers_quiesce(nullptr);  // DROPIN's td_evaluate keeps its own
     if (ch->engine != TD_ENGINE_DEVICE) {
         const int64_t t0 = now_ns();
         for (int64_t i = 0; i < iterations; ++i) {

@@ -299,7 +299,9 @@ int shadow_server_query_post(td_chain *ch, double x, double y, double z, const S
 int shadow_server_death_query(td_chain *ch, double x, double y, double z, double *val);
 int shadow_server_query_answer(td_chain *ch, double *val);
 int shadow_server_stop(td_chain *ch);
-// (servers_quiesce, which stops the thread's resident launches before other work: ctx.h)
+// Stop every resident server this thread runs except `keep` (nullable): called
+// before work on any other stream (chain.cpp t_servers).
+void servers_quiesce(const td_chain *keep);
 void shadow_server_diag(const td_chain *ch, int64_t out[4]);
 int shadow_profile(td_chain *ch, int64_t out[80]);
 // One-point Interpolation against the chain's model (edit == NULL) or that

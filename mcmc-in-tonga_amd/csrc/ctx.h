@@ -11,7 +11,6 @@
 
 namespace tdstar {
 struct td_shadow;
-struct EvalServer;
 }
 
 struct td_ctx {
@@ -78,10 +77,6 @@ struct td_ctx {
     // wait for them, [15] chi^2 and copy-out; [16] server busy, ns (the kernel's own clock), evaluate
     // commands, [17] the same, queries
     int64_t dropin_ns[18] = {};
-    // td_evaluate's full path as one resident launch (eval_server.h): created on first use
-    tdstar::EvalServer *evs = nullptr;
-    int eval_server_mode = 1;           // 0: always the three launches (tdt_eval_server_config)
-    int64_t eval_idle_us = 0, eval_guard_us = 0;  // testing overrides of its watchdogs (0: defaults)
     // td_misfit: device copies of the last (tS, sig) given and a pinned [ptS | phi] staging area
     double *mf_dev = nullptr;           // [ptS n | tS n | sig n | terms n | phi 1]
     double *mf_host = nullptr;          // pinned [ptS n | phi 1]
@@ -132,18 +127,7 @@ void shadow_free(td_ctx *ctx);
 // The shadow chain of td_evaluate's incremental path (nullptr if none).
 td_chain *shadow_chain_of(td_ctx *ctx);
 // Stop every resident server this thread runs except `keep` (chain.cpp).
-// keep_eval: a context whose resident full evaluate (eval_server.cpp) is kept too.
-void servers_quiesce(const td_chain *keep, const td_ctx *keep_eval = nullptr);
-// The resident full evaluate (eval_server.cpp): registered with the thread's resident launches.
-void resident_register_eval(td_ctx *ctx);
-void resident_unregister_eval(td_ctx *ctx);
-// another resident launch of this thread than ctx's own full evaluate is running
-bool resident_others(const td_ctx *ctx);
-// A grid-path full evaluate through the resident launch: *served = false when it does not apply (the
-// caller launches); ptS lands in ctx->h_out + 1.  issue_ns: the host time to post it.
-int eval_server_run(td_ctx *ctx, int64_t ncells, const CellGrid &G, bool *served, int64_t *issue_ns);
-int eval_server_stop(td_ctx *ctx);
-void eval_server_free(td_ctx *ctx);
+void servers_quiesce(const td_chain *keep);
 // td_interpolate of one point on the shadow's model (incremental.cpp); *handled = 0: not applicable.
 int interpolate_incremental(td_ctx *ctx, const double *x, const double *y, const double *z, const double *zeta,
                             int64_t ncells, double qx, double qy, double qz, double *val, int *handled);

@@ -29,9 +29,7 @@
 #include <climits>
 #include <cstdlib>
 
-#include "eval_server.h"
 #include "internal.h"
-#include "ray_sum.h"
 #include "wave_ops.h"
 
 namespace tdstar {
@@ -78,14 +76,6 @@ __global__ __launch_bounds__(256) void k_grid_fill(double *__restrict__ cells, c
     const int b = grid_bucket(G, x, y, z);
     const int pos = atomicAdd(&count[b], 1);  // order inside a bucket does not matter
     if (pos < kGridCap) ent[(long)b * kGridCap + pos] = BucketEntry{x, y, z, i, 0};
-}
-
-__device__ __forceinline__ long long ticks() { return (long long)wall_clock64(); }
-// the value v available (its load waited for) before whatever follows: the phase stamps
-__device__ __forceinline__ void depend(double v) { asm volatile("" ::"v"(v)); }
-__device__ __forceinline__ int wave_max_i(int v) {
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
 }
 
 // lexicographic min of (d, i) over each half-wave (32 lanes), to every lane
@@ -206,13 +196,18 @@ __device__ __forceinline__ void wave_lexmin(double &d, int &i) {
 // time: the 5x5x5 block (two buckets per lane), else every cell.
 constexpr int kGridLpp = 4;
 constexpr int64_t kGridQuadMinPts = 65536;  // below: the half-wave kernel (more waves, shorter chains)
-// The nearest cell of the lane's point (x, y, z) by its quad (4 lanes; all 64 lanes of the wave
-// active): (bd, bx) in every lane of the quad.  valid = false: a padding lane (proven at once).
-__device__ __forceinline__ void quad_nearest(double x, double y, double z, bool valid, const CellGrid &G,
-                                             const int *__restrict__ count, const BucketEntry *__restrict__ ent,
-                                             const double *__restrict__ cells, int stride, int ncells, double &bd,
-                                             int &bx, long long *stamp = nullptr) {
+__global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx, const double *__restrict__ qy,
+                                                  const double *__restrict__ qz, int npts, int ys, int zs, CellGrid G,
+                                                  const int *__restrict__ count, const BucketEntry *__restrict__ ent,
+                                                  const double *__restrict__ cells, int stride, int ncells,
+                                                  int *__restrict__ best_i, double *__restrict__ best_d,
+                                                  double *__restrict__ zeta0, int *__restrict__ other_count,
+                                                  int other_nb) {
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < other_nb; b += gridDim.x * blockDim.x) other_count[b] = 0;
     const int lane = threadIdx.x & 63, sub = threadIdx.x & (kGridLpp - 1);
+    const int p = (blockIdx.x * blockDim.x + threadIdx.x) / kGridLpp;  // whole quads stay for the DPP
+    const int pc = min(p, npts - 1);
+    const double x = qx[pc], y = qy[(long)pc * ys], z = qz[(long)pc * zs];
     const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
               bk = grid_axis(z, G.z0, G.iz, G.gz);
     constexpr int kMine = (27 + kGridLpp - 1) / kGridLpp;
@@ -230,12 +225,8 @@ __device__ __forceinline__ void quad_nearest(double x, double y, double z, bool 
         e[u] = ent[(long)bb[u] * kGridCap];
     }
     const double lb = grid_block_lb(G, x, y, z, 1);  // independent of the loads: computed while they fly
-    bd = kSentinel;
-    bx = INT_MAX;
-    if (stamp) {  // (diagnostics: the first round of loads back)
-        depend(e[kMine - 1].x + (double)cnt[kMine - 1]);
-        stamp[0] = ticks();
-    }
+    double bd = kSentinel;
+    int bx = INT_MAX;
 #pragma unroll
     for (int u = 0; u < kMine; ++u) {
         over = over || cnt[u] > kGridCap;
@@ -254,15 +245,9 @@ __device__ __forceinline__ void quad_nearest(double x, double y, double z, bool 
     quad_lexmin(bd, bx);
     const int qsh = lane & ~(kGridLpp - 1);  // first lane of my quad
     const bool any_over = ((__ballot(over) >> qsh) & 0xfull) != 0ull;
-    const bool proven = !valid || (!any_over && bd < lb);
+    const bool proven = p >= npts || (!any_over && bd < lb);
     // points the block does not prove: the whole wave, one at a time
     unsigned long long need = __ballot(!proven && sub == 0);
-    if (stamp) {
-        depend(bd);
-        stamp[1] = ticks();
-        stamp[2] = __popcll(need);
-        stamp[3] = __builtin_amdgcn_readfirstlane(wave_max_i(most));
-    }
     while (need) {
         const int src = __builtin_ctzll(need);
         need &= need - 1;
@@ -296,301 +281,11 @@ __device__ __forceinline__ void quad_nearest(double x, double y, double z, bool 
             bx = i2;
         }
     }
-    if (stamp) {
-        depend(bd);
-        stamp[4] = ticks();
-    }
-}
-
-__global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx, const double *__restrict__ qy,
-                                                  const double *__restrict__ qz, int npts, int ys, int zs, CellGrid G,
-                                                  const int *__restrict__ count, const BucketEntry *__restrict__ ent,
-                                                  const double *__restrict__ cells, int stride, int ncells,
-                                                  int *__restrict__ best_i, double *__restrict__ best_d,
-                                                  double *__restrict__ zeta0, int *__restrict__ other_count,
-                                                  int other_nb) {
-    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < other_nb; b += gridDim.x * blockDim.x) other_count[b] = 0;
-    const int sub = threadIdx.x & (kGridLpp - 1);
-    const int p = (blockIdx.x * blockDim.x + threadIdx.x) / kGridLpp;  // whole quads stay for the DPP
-    const int pc = min(p, npts - 1);
-    const double x = qx[pc], y = qy[(long)pc * ys], z = qz[(long)pc * zs];
-    double bd;
-    int bx;
-    quad_nearest(x, y, z, p < npts, G, count, ent, cells, stride, ncells, bd, bx);
     if (sub == 0 && p < npts) {
         const bool found = bd < kSentinel;
         best_i[p] = found ? bx : -1;
         if (best_d) best_d[p] = bd;
         if (zeta0) zeta0[p] = found ? cells[3 * (long)stride + bx] : 0.0;  // MCsub.jl:249
-    }
-}
-
-// ---- td_evaluate's full path as one resident launch (eval_server.h) ----
-
-// pinned host memory: system-scope atomics (coherent, never served from a stale cache line)
-__device__ __forceinline__ long long sys_load(const long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void sys_store(long long *p, long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ long long readlane_i64(long long v, int l) {
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(unsigned long long)v, l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)v >> 32), l);
-    return (long long)(((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ int sgpr_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ double sgpr_d(double v) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-// the workgroup's points' zeta0 in LDS, addressed by global point index
-struct LdsZeta {
-    const double *z;
-    int p0;
-    __device__ __forceinline__ double operator()(int k) const { return z[k - p0]; }
-};
-
-enum : int { kEvalGo = 0, kEvalStop = 1, kEvalFail = 2 };
-
-// Wave 0 of each workgroup: the next command into cmd (LDS, EvalCmd's bytes); the outcome in *state.
-// Workgroup 0 polls the mailbox (every word in one round trip, taken when its check matches) and
-// forwards the words as {word, tag} granules: 8-byte agent-scope atomics, each whole or not at all,
-// so a reader that sees every granule with the new tag has the whole command with no further
-// ordering.  The others poll the granules.  Workgroup 0 alone quits on silence: it marks the launch
-// exited (the host then knows it took nothing more), then forwards a QUIT.
-__device__ __forceinline__ void eval_take(const EvalArgs &A, long long last, unsigned *cmd, int *state, int lane,
-                                          long long *t_take) {
-    constexpr int W = kEvalCmdWords, G2 = 2 * kEvalCmdWords;
-    const long long t0 = ticks();
-    if (blockIdx.x == 0) {
-        while (true) {
-            const long long w = lane < W ? sys_load(reinterpret_cast<const long long *>(A.mb) + lane) : 0;
-            const long long sq = readlane_i64(w, 0);
-            bool fresh = sq != last;
-            if (fresh) {  // (a poll that caught the host between its words: polled again)
-                const unsigned long long h = wave_xor_u64(
-                    lane >= 1 && lane < W - 1 ? eval_mix((unsigned long long)w, lane, sq) : 0ull);
-                fresh = h == (unsigned long long)readlane_i64(w, W - 1);
-            }
-            const bool idle = !fresh && ticks() - t0 > A.idle_ticks;
-            if (fresh || idle) {
-                long long v = w;
-                if (idle) {  // the QUIT forwarded to the others: seq last + 1, type kEvalQuit
-                    v = lane == 0 ? last + 1 : (lane == 1 ? (long long)kEvalQuit : 0);
-                    if (lane == 0) sys_store(&A.ctl->exited, 1);
-                }
-                const unsigned long long tag = (unsigned long long)eval_tag(readlane_i64(v, 0)) << 32;
-                if (lane < W) {
-                    __hip_atomic_store(&A.bcast[2 * lane], tag | (unsigned)(unsigned long long)v, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&A.bcast[2 * lane + 1], tag | (unsigned)((unsigned long long)v >> 32),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    cmd[2 * lane] = (unsigned)(unsigned long long)v;
-                    cmd[2 * lane + 1] = (unsigned)((unsigned long long)v >> 32);
-                }
-                if (lane == 0) {
-                    *t_take = ticks();
-                    if (fresh) sys_store(&A.ctl->t_take, *t_take);
-                    *state = idle ? kEvalStop : (readlane_i64(v, 1) & 0xffffffff) == kEvalRun ? kEvalGo : kEvalStop;
-                }
-                return;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    const unsigned expect = eval_tag(last + 1);
-    while (true) {
-        const unsigned long long g =
-            lane < G2 ? __hip_atomic_load(&A.bcast[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : (unsigned long long)expect << 32;
-        if (__ballot((unsigned)(g >> 32) != expect) == 0ull) {
-            if (lane < G2) cmd[lane] = (unsigned)g;
-            const int type = __builtin_amdgcn_readlane((int)(unsigned)g, 2);  // word 1's low half
-            if (lane == 0) {
-                *t_take = ticks();
-                *state = type == kEvalRun ? kEvalGo : kEvalStop;
-            }
-            return;
-        }
-        // workgroup 0 gone without a QUIT reaching this one (it failed): leave after twice its watchdog
-        if (ticks() - t0 > 2 * A.idle_ticks + A.guard_ticks) {
-            if (lane == 0) *state = kEvalStop;
-            return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-__global__ __launch_bounds__(kEvalThreads) void k_eval_server(const EvalArgs A) {
-    extern __shared__ double zsh[];  // [lds_pts]: the zeta0 of this workgroup's points
-    __shared__ double scratch[kEvalThreads / 64][96];
-    __shared__ __attribute__((aligned(16))) unsigned cmd[2 * kEvalCmdWords];
-    __shared__ int state;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wg = blockIdx.x;
-    const int r0 = A.wg_ray[wg], r1 = A.wg_ray[wg + 1];
-    const int p0 = A.ray_off[r0], p1 = A.ray_off[r1];
-    const int shard = wg & 7;
-    const unsigned in_shard = (unsigned)((A.nwg - shard + 7) / 8);  // workgroups w with w % 8 == shard
-    unsigned *fin = A.arrive + 8 * 32;                               // the finish shards, after the arrival ones
-    long long last = A.seq0;
-    unsigned k = 0;  // commands run by this launch (the grid barrier's target is k * nwg arrivals)
-    long long st[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // phase stamps (tid 0; EvalStamps)
-    while (true) {
-        if (wv == 0) eval_take(A, last, cmd, &state, lane, &st[0]);
-        __syncthreads();
-        if (state != kEvalGo) break;
-        const EvalCmd &c = *reinterpret_cast<const EvalCmd *>(cmd);
-        const long long seq = readlane_i64(c.seq, 0);
-        const int ncells = sgpr_i(c.ncells), stride = sgpr_i(c.stride), par = sgpr_i(c.par);
-        const int other_nb = sgpr_i(c.other_nb), diag = sgpr_i(c.diag);
-        // (through address space 1: global_ loads and stores, not flat_ ones, which LDS waits would count)
-        using gdouble = __attribute__((address_space(1))) double;
-        double *cells = (double *)(gdouble *)readlane_i64(reinterpret_cast<long long>(c.cells), 0);
-        const double *stage = (const double *)(const gdouble *)readlane_i64(reinterpret_cast<long long>(c.stage), 0);
-        CellGrid G;
-        G.gx = sgpr_i(c.G.gx), G.gy = sgpr_i(c.G.gy), G.gz = sgpr_i(c.G.gz);
-        G.x0 = sgpr_d(c.G.x0), G.y0 = sgpr_d(c.G.y0), G.z0 = sgpr_d(c.G.z0);
-        G.ix = sgpr_d(c.G.ix), G.iy = sgpr_d(c.G.iy), G.iz = sgpr_d(c.G.iz);
-        G.hx = sgpr_d(c.G.hx), G.hy = sgpr_d(c.G.hy), G.hz = sgpr_d(c.G.hz);
-        G.ex = sgpr_d(c.G.ex), G.ey = sgpr_d(c.G.ey), G.ez = sgpr_d(c.G.ez);
-        for (int a = 0; a < 3; ++a) {
-            G.lo[a] = sgpr_d(c.G.lo[a]);
-            G.hi[a] = sgpr_d(c.G.hi[a]);
-        }
-        G.sealed = sgpr_i(c.G.sealed);
-        last = seq;
-        ++k;
-        int *count = A.count + (long)par * kGridMaxBuckets;
-        int *other = A.count + (long)(par ^ 1) * kGridMaxBuckets;
-        // ---- fill: this workgroup's share of the cells into their buckets (k_grid_fill) ----
-        const int per = (ncells + A.nwg - 1) / A.nwg;
-        const int c1 = min(ncells, (wg + 1) * per);
-#ifndef TD_EVS_STAGE
-#define TD_EVS_STAGE 0
-#endif
-#if TD_EVS_STAGE == 1
-        if (wg * per < c1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (system scope: stale staged lines out)
-#endif
-        for (int i = wg * per + tid; i < c1; i += kEvalThreads) {
-#if TD_EVS_STAGE == 0
-            const double x = __longlong_as_double(sys_load(reinterpret_cast<const long long *>(stage + i)));
-            const double y = __longlong_as_double(sys_load(reinterpret_cast<const long long *>(stage + stride + i)));
-            const double z =
-                __longlong_as_double(sys_load(reinterpret_cast<const long long *>(stage + 2 * (long)stride + i)));
-            const double ze =
-                __longlong_as_double(sys_load(reinterpret_cast<const long long *>(stage + 3 * (long)stride + i)));
-#else
-            const double x = stage[i], y = stage[stride + i], z = stage[2 * (long)stride + i],
-                         ze = stage[3 * (long)stride + i];
-#endif
-            if (diag && tid == 0) {
-                depend(x + y + z + ze);
-                st[1] = ticks();
-            }
-            cells[i] = x;
-            cells[stride + i] = y;
-            cells[2 * (long)stride + i] = z;
-            cells[3 * (long)stride + i] = ze;
-            const int b = grid_bucket(G, x, y, z);
-            const int pos = atomicAdd(&count[b], 1);  // order inside a bucket does not matter
-            if (diag && tid == 0) {
-                depend((double)pos);
-                st[2] = ticks();
-            }
-            if (pos < kGridCap) A.ent[(long)b * kGridCap + pos] = BucketEntry{x, y, z, i, 0};
-        }
-        // the previous evaluate's counts zeroed for the next one (ordered before it by this barrier)
-        const int zper = (other_nb + A.nwg - 1) / A.nwg;
-        const int z1 = min(other_nb, (wg + 1) * zper);
-        for (int b = wg * zper + tid; b < z1; b += kEvalThreads) other[b] = 0;
-        // ---- grid barrier: every store above, from every workgroup, before any search ----
-        // (cdna_hip_programming.md Guideline 16: stores drained, workgroup barrier, one agent release,
-        // drained again, then the arrival; the waiter's one agent acquire before the workgroup barrier)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            st[3] = ticks();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            st[4] = ticks();
-            __hip_atomic_fetch_add(&A.arrive[shard * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (wv == 0) {
-            const unsigned target = k * (unsigned)A.nwg;
-            const long long t0 = ticks();
-            bool fail = false;
-            while (true) {
-                const unsigned v =
-                    lane < 8 ? __hip_atomic_load(&A.arrive[lane * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-                unsigned s = 0;
-#pragma unroll
-                for (int l = 0; l < 8; ++l) s += (unsigned)__builtin_amdgcn_readlane((int)v, l);
-                if ((int)(s - target) >= 0) break;  // (wraps with the counters)
-                if (ticks() - t0 > A.guard_ticks) {
-                    fail = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0 && fail) state = kEvalFail;
-        }
-        __syncthreads();
-        if (tid == 0) st[5] = ticks();
-        if (state == kEvalFail) {  // abandoned: the host takes the launches (and this launch ends)
-            if (tid == 0) {
-                sys_store(&A.ctl->failed, seq);
-                if (wg == 0) sys_store(&A.ctl->exited, 1);
-            }
-            break;
-        }
-        // ---- search: the points of this workgroup's rays, 16 per wave (k_nn_grid4's quads) ----
-        for (int base = p0 + wv * 16; base < p1; base += kEvalThreads / 4) {
-            const int p = base + (lane >> 2);
-            const int pc = min(p, p1 - 1);
-            double bd;
-            int bx;
-            quad_nearest(A.px[pc], A.py[pc], A.pz[pc], p < p1, G, count, A.ent, cells, stride, ncells, bd, bx,
-                         diag && wv == 0 && base == p0 ? &st[10] : nullptr);
-            const double zv = bd < kSentinel ? cells[3 * (long)stride + bx] : 0.0;  // MCsub.jl:249
-            if ((lane & 3) == 0 && p < p1) zsh[p - p0] = zv;
-            if (diag && tid == 0 && base == p0) {
-                depend(zv);
-                st[6] = ticks();
-            }
-        }
-        __syncthreads();
-        if (tid == 0) st[7] = ticks();
-        // ---- ray sums: one wave per ray (ray_sum.h), ptS straight into pinned memory ----
-        for (int r = r0 + wv; r < r1; r += kEvalThreads / 64) {
-            const int s0 = A.ray_off[r];
-            const double v = wave_ray_sum(lane, A.w, LdsZeta{zsh, p0}, s0, A.ray_off[r + 1] - s0, scratch[wv]);
-            if (lane == 0) {
-                A.ptS[r] = v;
-                sys_store(reinterpret_cast<long long *>(A.ptS_host + r), __double_as_longlong(v));
-            }
-        }
-        if (tid == 0) st[8] = ticks();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every reply word acknowledged before done
-        __syncthreads();
-        if (tid == 0) {
-            st[9] = ticks();
-            if (diag) {
-                for (int j = 0; j < 15; ++j) sys_store(&A.stamps[wg].t[j], st[j]);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            // the shard's last workgroup (its add returns the shard's full count) tells the host
-            const unsigned old = __hip_atomic_fetch_add(&fin[shard * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old + 1u == k * in_shard) {
-                sys_store(&A.ctl->t_end[shard], ticks());
-                sys_store(&A.ctl->done[shard], seq);
-            }
-        }
     }
 }
 
@@ -650,17 +345,6 @@ hipError_t launch_nearest_grid(const double *qx, const double *qy, const double 
         work.g_par = par ^ 1;
     }
     return e;
-}
-
-}  // namespace tdstar
-
-namespace tdstar {
-
-hipError_t launch_eval_server(const EvalArgs &a, hipStream_t s) {
-    if (a.nwg <= 0 || a.lds_pts <= 0 || a.lds_pts > kEvalMaxLdsPts) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_eval_server, dim3((unsigned)a.nwg), dim3(kEvalThreads), sizeof(double) * (size_t)a.lds_pts,
-                       s, a);
-    return hipGetLastError();
 }
 
 }  // namespace tdstar
