@@ -166,5 +166,12 @@ _ARRAY_PTRS = (_pd, _pi32, _pi64, _pu32)
 
 def ptr(a, t=_pd):
     """The address of a C-contiguous numpy array (the declared element type `t` is documentation:
-    callers convert with f64() / np.int32 / np.int64 first), or None."""
-    return a.__array_interface__["data"][0] if a is not None else None
+    callers convert with f64() / np.int32 / np.int64 first), or None.  Through the buffer protocol
+    (0.3 us) where the array is writable; `__array_interface__` builds a dict per call (1.2 us, five
+    of them per td_evaluate)."""
+    if a is None:
+        return None
+    try:
+        return ctypes.addressof(ctypes.c_char.from_buffer(a))
+    except (TypeError, ValueError, BufferError):  # read-only or empty: the array interface
+        return a.__array_interface__["data"][0]
