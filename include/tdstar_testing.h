@@ -91,6 +91,15 @@ int tdt_set_server_post_delay(int ms);
  * runs each round once, with the results of an undisturbed launch.  One-shot;
  * ends the running launch. */
 int tdt_rounds_force_exit(td_rounds *r, const int32_t *slots, int64_t nslots);
+/* Testing: the drop-in path's one-point Interpolation on the host (host_nn.h: MCsub.jl:247-263 over a
+ * bucket grid of the committed model).  Builds the grid from the n cells, applies edits[0..nedits) as
+ * committed (6 doubles each: action 1 birth / 2 death / 3 change / 4 move, 0-based Julia index, x, y, z,
+ * zeta), then answers nq points on that model plus `pending` (6 doubles, or NULL): val_out[k] and, if
+ * pos_out, the winner's 0-based Julia position (-1: no cell below the 1e9 sentinel).  Host only. */
+int tdt_host_nn_query(const double *x, const double *y, const double *z, const double *zeta, int64_t n,
+                      const double *edits, int64_t nedits, const double *pending, const double *qx,
+                      const double *qy, const double *qz, int64_t nq, double *val_out, int64_t *pos_out);
+
 /* Diagnostic: the drop-in path's wall time per stage, ns, accumulated on the
  * context (then zeroed if reset): [0] td_evaluate, [1] its model
  * classification (which state the caller's cells are an edit of), [2] its

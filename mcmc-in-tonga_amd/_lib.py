@@ -112,6 +112,7 @@ SIGNATURES = {
     "tdt_set_server_post_delay": (ctypes.c_int, [ctypes.c_int]),
     "tdt_rounds_force_exit": (ctypes.c_int, [_vp, _pi32, _i64]),
     "tdt_dropin_timing": (ctypes.c_int, [_vp, ctypes.c_int, _pi64]),
+    "tdt_host_nn_query": (ctypes.c_int, [_pd, _pd, _pd, _pd, _i64, _pd, _i64, _pd, _pd, _pd, _pd, _i64, _pd, _pi64]),
     "tdt_shadow_diag": (ctypes.c_int, [_vp, _pi64]),
     "tdt_shadow_profile": (ctypes.c_int, [_vp, _pi64]),
     "tdt_chi2": (ctypes.c_int, [_vp, _pd, ctypes.c_int, _pd]),

@@ -21,11 +21,13 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "chain_dev.h"
 #include "ctx.h"
+#include "host_nn.h"
 
 namespace tdstar {
 
@@ -55,6 +57,7 @@ struct Cells {
 struct td_shadow {
     td_chain *ch = nullptr;
     Cells B;                 // committed model (Julia order), what the shadow chain holds
+    HostNN nn;               // B's cells in a host bucket grid: one-point Interpolation queries (host_nn.h)
     double phiB = 0.0;
     std::vector<double> ptSB;
     std::vector<double> preB;  // B's chi^2 partial sums (MCsub.jl:169-172): phi_n is formed here, from them
@@ -381,6 +384,21 @@ bool all_sane(const double *const in[4], int64_t n) {
     return true;
 }
 
+// Julia went on from Q: the committed model takes the pending edit (host copy and host grid)
+void commit_q(td_shadow *s) {
+    s->B.apply(s->e);
+    s->nn.apply(s->e);
+}
+
+// TD_HOST_QUERY=0: one-point queries go to the device server as before (A/B measurements)
+bool host_query_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("TD_HOST_QUERY");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 void drop_chain(td_shadow *s) {
     if (s->ch) shadow_chain_destroy(s->ch);
     s->ch = nullptr;
@@ -405,6 +423,7 @@ int build_shadow(td_ctx *ctx, td_shadow *s) {
     int rc = shadow_chain_create(ctx, c.x.data(), c.y.data(), c.z.data(), c.zeta.data(), n, cap, box, &s->ch);
     if (rc) return rc;
     s->B = c;
+    s->nn.build(c.x.data(), c.y.data(), c.z.data(), c.zeta.data(), n);
     s->phiB = s->last_phi;
     s->ptSB = s->last_ptS;
     chi2_resume(ctx, s->ptSB.data(), 0, s->preB, s->preB);  // (== phiB: the same sequential sum)
@@ -478,7 +497,7 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
                     c.decision = 1;
                     steps[nsteps++] = c;
                 }
-                s->B.apply(s->e);
+                commit_q(s);
                 s->phiB = s->phiQ;
                 s->ptSB.swap(s->ptSQ);
                 s->preB.swap(s->preQ);
@@ -557,7 +576,7 @@ int evaluate_incremental(td_ctx *ctx, const double *x, const double *y, const do
             c.decision = 1;  // re-evaluate and commit Q first
             steps[nsteps++] = c;
         }
-        s->B.apply(s->e);  // B := Q (in place: O(1) but for a death's shift)
+        commit_q(s);  // B := Q (in place: O(1) but for a death's shift)
         s->phiB = s->phiQ;
         s->ptSB.swap(s->ptSQ);
         s->preB.swap(s->preQ);
@@ -609,6 +628,18 @@ int interpolate_incremental(td_ctx *ctx, const double *x, const double *y, const
     if (!s || !s->ch || !std::isfinite(qx) || !std::isfinite(qy) || !std::isfinite(qz)) return TD_OK;
     const double *in[4] = {x, y, z, zeta};
     ScriptStep e2;
+    if (host_query_on()) {
+        // the cells must be B or Q bit for bit (one scan); then the host grid answers (host_nn.h) and the
+        // device -- its pending proposal untouched -- never sees the call
+        const int64_t tc = now_ns();
+        const int rb = classify(in, M, View(s->B, nullptr), &e2);
+        const bool on_b = rb == 0, on_q = rb == 1 && s->pending && std::memcmp(&e2, &s->e, sizeof e2) == 0;
+        ctx->dropin_ns[4] += now_ns() - tc;
+        if (!on_b && !on_q) return TD_OK;  // another model: the plain path answers
+        *val = s->nn.query(qx, qy, qz, on_q ? &s->e : nullptr);
+        *handled = 1;
+        return TD_OK;
+    }
     if (s->dev_pending && !shadow_server_alive(s->ch)) s->dev_pending = false;
     if (shadow_server_alive(s->ch)) {
         // a running server: post the query on the model the cells most likely are (the pending proposal
@@ -665,5 +696,45 @@ extern "C" int tdt_shadow_diag(td_ctx *ctx, int64_t out[4]) {
     if (!ctx || !out) return TD_ERR_ARG;
     for (int k = 0; k < 4; ++k) out[k] = 0;
     if (ctx->shadow && ctx->shadow->ch) tdstar::shadow_server_diag(ctx->shadow->ch, out);
+    return TD_OK;
+}
+
+extern "C" int tdt_host_nn_query(const double *x, const double *y, const double *z, const double *zeta, int64_t n,
+                                 const double *edits, int64_t nedits, const double *pending, const double *qx,
+                                 const double *qy, const double *qz, int64_t nq, double *val_out, int64_t *pos_out) {
+    if (n < 0 || nedits < 0 || nq < 0 || (n > 0 && (!x || !y || !z || !zeta)) || (nedits > 0 && !edits) ||
+        (nq > 0 && (!qx || !qy || !qz || !val_out)))
+        return TD_ERR_ARG;
+    auto step = [](const double *r) {
+        tdstar::ScriptStep e{};
+        e.action = (int)r[0];
+        e.index = (int)r[1];
+        e.x = r[2], e.y = r[3], e.z = r[4], e.zeta = r[5];
+        return e;
+    };
+    tdstar::HostNN nn;
+    nn.build(x, y, z, zeta, n);
+    int64_t size = n;
+    auto valid = [&](const tdstar::ScriptStep &e) {
+        if (e.action < 1 || e.action > 4) return false;
+        if (e.action != 1 && (e.index < 0 || e.index >= size)) return false;
+        return !(e.action == 2 && size < 1);
+    };
+    for (int64_t k = 0; k < nedits; ++k) {
+        const tdstar::ScriptStep e = step(edits + 6 * k);
+        if (!valid(e)) return TD_ERR_ARG;
+        nn.apply(e);
+        size += e.action == 1 ? 1 : e.action == 2 ? -1 : 0;
+    }
+    tdstar::ScriptStep pe{};
+    if (pending) {
+        pe = step(pending);
+        if (!valid(pe)) return TD_ERR_ARG;
+    }
+    for (int64_t k = 0; k < nq; ++k) {
+        int64_t pos = -1;
+        val_out[k] = nn.query(qx[k], qy[k], qz[k], pending ? &pe : nullptr, &pos);
+        if (pos_out) pos_out[k] = pos;
+    }
     return TD_OK;
 }
