@@ -172,7 +172,7 @@ class HostNN {
     int coord(int a, double v) const {
         if (nb_[a] == 1) return 0;
         double t = std::floor((v - lo_[a]) * inv_[a]);
-        t = std::min(std::max(t, 0.0), (double)(nb_[a] - 1));
+        t = t >= 0.0 ? std::min(t, (double)(nb_[a] - 1)) : 0.0;  // (NaN: bucket 0; its distances never count)
         return (int)t;
     }
     int bucket_of(double x, double y, double z) const { return (coord(2, z) * nb_[1] + coord(1, y)) * nb_[0] + coord(0, x); }

@@ -115,7 +115,8 @@ def test_sentinel(tt, orc):
     x = np.array([0.0, r, np.nextafter(r, 0), 2 * r, 50.0])
     cells = [x, np.zeros(5), np.zeros(5), np.array([1.0, 2.0, 3.0, 4.0, 5.0])]
     Q = np.array([[0.0, 0, 0], [-r, 0, 0], [-np.nextafter(r, 0), 0, 0], [-1e6, 0, 0], [3 * r, 0, 0],
-                  [r / 2, r, r], [1e7, 1e7, 1e7], [r + 50.0, 0, 0], [0.0, -r, 0]])
+                  [r / 2, r, r], [1e7, 1e7, 1e7], [r + 50.0, 0, 0], [0.0, -r, 0],
+                  [np.nan, 0, 0], [np.inf, 0, 0], [-np.inf, 1.0, 1.0], [0.0, np.nan, np.inf]])
     check(tt, orc, cells, [], None, Q)
     check(tt, orc, cells, [[2, 0, 0, 0, 0, 0]], None, Q)
     check(tt, orc, cells, [], [4, 4, -3e4, 0.0, 0.0, 0], Q)
