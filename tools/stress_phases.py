@@ -21,5 +21,5 @@ cyc = d[:7].copy(); cyc[6] += d[12] + d[13]
 names = ["top", "B", "C", "D", "E", "F", "G"]
 out = {"us_per_prop": el / n * 1e6, "cycles": {k: round(v / n, 1) for k, v in zip(names, cyc)}, "total": round(cyc.sum() / n, 1),
        "by_action": {nm: {"share": round(prop[i] / max(prop.sum(), 1), 3), **{p: round(x, 1) for p, x in zip(("top", "B", "C", "D", "E", "F", "G12", "G13", "G"), d[16 + 10 * i: 16 + 10 * i + 9] / max(prop[i], 1))}} for i, nm in enumerate(("birth", "death", "change", "move"))},
-       "diag": {k: round(d[k] / n, 3) for k in (14, 64, 65, 66, 67, 68, 69, 70, 71)}}
+       "diag": {k: round(d[k] / n, 3) for k in (14, 15, 64, 65, 66, 67, 68, 69, 70, 71)}}
 print(json.dumps(out, indent=1))
