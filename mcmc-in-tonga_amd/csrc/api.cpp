@@ -266,7 +266,9 @@ int evaluate_full(td_ctx *ctx, const double *x, const double *y, const double *z
     const int64_t t1 = now_ns();
     const auto &g = ctx->g;
     Timer *tm = ctx->timer.on ? &ctx->timer : nullptr;
-    hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, ncells, ctx->best_i, ctx->best_d, ctx->zeta0);
+    // (the indices only when asked for, the distances never: td_evaluate needs each point's value)
+    hipError_t e = nearest_uploaded(ctx, g.px, g.py, g.pz, g.P, 1, 1, ncells, nearest_out ? ctx->best_i : nullptr,
+                                    nullptr, ctx->zeta0);
     if (e != hipSuccess) return hip_err(ctx, e, "nearest kernels");
     // ptS lands in pinned host memory straight from the kernel (no copy back)
     e = launch_ray_sums(g, ctx->zeta0, ctx->ptS, ctx->stream, tm, ctx->h_out_dev + 1);

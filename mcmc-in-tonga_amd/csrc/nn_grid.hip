@@ -7,7 +7,8 @@
 // sentinel -- v_nearest's strict '<' scan in index order keeps the FIRST
 // minimum.  The grid only decides where to look:
 //   k_grid_fill  one lane per cell: append {x, y, z, index} to its bucket
-//                (kGridCap entries; a fuller bucket is flagged);
+//                (kGridCap entries, the first two of every bucket side by side
+//                -- grid_ent; a fuller bucket is flagged);
 //   k_nn_grid    32 lanes per point, one per bucket of the 3x3x3 block
 //                around it, DPP reduction; the answer counts only if it is
 //                strictly closer than every face of the block
@@ -53,6 +54,14 @@ __device__ __forceinline__ void take(double d, int i, double &bd, int &bi) {
     }
 }
 
+// Entry k of bucket b: the first kGridHead entries of every bucket sit together, densely (a bucket
+// holds ~2 cells, so a search's one round of loads reads 64 B per bucket and two buckets share a
+// 128-B line), the rest in a per-bucket overflow area after them.  nb = the grid's bucket count.
+constexpr int kGridHead = 2;
+__device__ __forceinline__ long grid_ent(long b, int k, long nb) {
+    return k < kGridHead ? b * kGridHead + k : nb * kGridHead + b * kGridCap + k;
+}
+
 __global__ __launch_bounds__(256) void k_grid_fill(double *__restrict__ cells, const double *__restrict__ stage,
                                                    int stride, int ncells, CellGrid G, int *__restrict__ count,
                                                    BucketEntry *__restrict__ ent) {
@@ -75,7 +84,7 @@ __global__ __launch_bounds__(256) void k_grid_fill(double *__restrict__ cells, c
     }
     const int b = grid_bucket(G, x, y, z);
     const int pos = atomicAdd(&count[b], 1);  // order inside a bucket does not matter
-    if (pos < kGridCap) ent[(long)b * kGridCap + pos] = BucketEntry{x, y, z, i, 0};
+    if (pos < kGridCap) ent[grid_ent(b, pos, (long)G.gx * G.gy * G.gz)] = BucketEntry{x, y, z, i, 0};
 }
 
 // lexicographic min of (d, i) over each half-wave (32 lanes), to every lane
@@ -117,6 +126,7 @@ __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, 
     const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
               bk = grid_axis(z, G.z0, G.iz, G.gz);
     const double *zeta_cells = cells + 3 * (long)stride;
+    const long nbk_all = (long)G.gx * G.gy * G.gz;
     double bd = kSentinel;
     int bx = INT_MAX;
     bool proven = false;
@@ -133,11 +143,11 @@ __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, 
             const long b = inb ? ((long)kk * G.gy + jj) * G.gx + ii : 0;
             // one round of loads: the count and the first two entries
             const int cnt = inb ? count[b] : 0;
-            const BucketEntry e0 = ent[b * kGridCap], e1 = ent[b * kGridCap + 1];
+            const BucketEntry e0 = ent[grid_ent(b, 0, nbk_all)], e1 = ent[grid_ent(b, 1, nbk_all)];
             if (cnt > 0) take(dist2_q(e0.x, e0.y, e0.z, x, y, z), e0.slot, bd, bx);
             if (cnt > 1) take(dist2_q(e1.x, e1.y, e1.z, x, y, z), e1.slot, bd, bx);
             for (int k = 2; k < min(cnt, kGridCap); ++k) {
-                const BucketEntry e = ent[b * kGridCap + k];
+                const BucketEntry e = ent[grid_ent(b, k, nbk_all)];
                 take(dist2_q(e.x, e.y, e.z, x, y, z), e.slot, bd, bx);
             }
             over = over || cnt > kGridCap;
@@ -156,7 +166,7 @@ __global__ __launch_bounds__(256) void k_nn_grid(const double *__restrict__ qx, 
     }
     if (hl == 0 && p < npts) {
         const bool found = bd < kSentinel;
-        best_i[p] = found ? bx : -1;
+        if (best_i) best_i[p] = found ? bx : -1;
         if (best_d) best_d[p] = bd;
         if (zeta0) zeta0[p] = found ? zeta_cells[bx] : 0.0;  // MCsub.jl:249
     }
@@ -211,6 +221,7 @@ __global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx,
     const int bi = grid_axis(x, G.x0, G.ix, G.gx), bj = grid_axis(y, G.y0, G.iy, G.gy),
               bk = grid_axis(z, G.z0, G.iz, G.gz);
     constexpr int kMine = (27 + kGridLpp - 1) / kGridLpp;
+    const long nbk_all = (long)G.gx * G.gy * G.gz;
     int bb[kMine], cnt[kMine];
     BucketEntry e[kMine];
     bool over = false;
@@ -222,7 +233,7 @@ __global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx,
         const bool inb = t < 27 && ii >= 0 && ii < G.gx && jj >= 0 && jj < G.gy && kk >= 0 && kk < G.gz;
         bb[u] = inb ? (kk * G.gy + jj) * G.gx + ii : 0;
         cnt[u] = inb ? count[bb[u]] : 0;
-        e[u] = ent[(long)bb[u] * kGridCap];
+        e[u] = ent[grid_ent(bb[u], 0, nbk_all)];
     }
     const double lb = grid_block_lb(G, x, y, z, 1);  // independent of the loads: computed while they fly
     double bd = kSentinel;
@@ -237,7 +248,7 @@ __global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx,
     for (int k = 1; k < most; ++k) {  // entry k of each of my buckets: one round of loads
 #pragma unroll
         for (int u = 0; u < kMine; ++u)
-            if (k < cnt[u]) e[u] = ent[(long)bb[u] * kGridCap + k];
+            if (k < cnt[u]) e[u] = ent[grid_ent(bb[u], k, nbk_all)];
 #pragma unroll
         for (int u = 0; u < kMine; ++u)
             if (k < cnt[u]) take(dist2_q(e[u].x, e[u].y, e[u].z, x, y, z), e[u].slot, bd, bx);
@@ -264,7 +275,7 @@ __global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx,
             const int c = count[b];
             over2 = over2 || c > kGridCap;
             for (int k = 0; k < min(c, kGridCap); ++k) {
-                const BucketEntry f = ent[(long)b * kGridCap + k];
+                const BucketEntry f = ent[grid_ent(b, k, nbk_all)];
                 take(dist2_q(f.x, f.y, f.z, px, py, pz), f.slot, d2, i2);
             }
         }
@@ -283,7 +294,7 @@ __global__ __launch_bounds__(256) void k_nn_grid4(const double *__restrict__ qx,
     }
     if (sub == 0 && p < npts) {
         const bool found = bd < kSentinel;
-        best_i[p] = found ? bx : -1;
+        if (best_i) best_i[p] = found ? bx : -1;
         if (best_d) best_d[p] = bd;
         if (zeta0) zeta0[p] = found ? cells[3 * (long)stride + bx] : 0.0;  // MCsub.jl:249
     }
@@ -314,7 +325,7 @@ hipError_t launch_nearest_grid(const double *qx, const double *qy, const double 
         work.g_par = 0;
         work.g_used[0] = work.g_used[1] = 0;
     }
-    grow(reinterpret_cast<void *&>(work.g_ent), work.g_ent_cap, sizeof(BucketEntry) * (size_t)nb * kGridCap);
+    grow(reinterpret_cast<void *&>(work.g_ent), work.g_ent_cap, sizeof(BucketEntry) * (size_t)nb * (kGridHead + kGridCap));
     if (e != hipSuccess) return e;
     const int64_t half = (int64_t)(work.g_count_cap / (2 * sizeof(int)));
     const int par = work.g_par;
