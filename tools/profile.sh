@@ -20,6 +20,7 @@ trace_only() {  # name, bench args...: kernel trace only (PMC passes serialize t
 mkdir -p $OUT/single $OUT/many $OUT/packed $OUT/stress $OUT/config4
 if [ -n "$2" ]; then  # one pass only: tools/profile.sh TAG stress
     [ "$2" = stress ] && { run stress --steps 1 --warmup 0 --iters-per-step 10 --no-cpu-baseline --no-full-evaluate --no-dropin --no-config4 --batch-chains 0 || exit 1; }
+    [ "$2" = single ] && { run single --steps 3 --warmup 1 --no-cpu-baseline --batch-chains 0 --no-stress --no-dropin --no-config4 || exit 1; }
     exit 0
 fi
 run single --steps 3 --warmup 1 --no-cpu-baseline --batch-chains 0 --no-stress --no-dropin --no-config4 && \
