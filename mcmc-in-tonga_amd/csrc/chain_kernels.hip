@@ -1235,10 +1235,14 @@ constexpr double kSumSlack = 2.3e-16;
 // *phi_n.  `overlay`: a proposal's terms are in place (its rays flagged, their
 // committed terms in cterm), staged through cprefix.  Out of line: it is
 // rare, and the kernel is at its register limit.
-// (The arrays by value: a Views passed by reference would be spilled to scratch in the caller.)
-__device__ __attribute__((noinline)) double exact_sums(const double *term, double *prefix, double *cprefix,
-                                                       const double *cterm, const int *rflag, Shared &sh, int n,
-                                                       int lane, bool overlay, int k0, double phi, double *phi_n) {
+// (The arrays by value: a Views passed by reference would be spilled to scratch in the caller; phi_n
+// comes back in the result for the same reason -- an out-pointer would keep the caller's phi_n in scratch.)
+struct ExactPhis {
+    double phi, phi_n;
+};
+__device__ __attribute__((noinline)) ExactPhis exact_sums(const double *term, double *prefix, double *cprefix,
+                                                          const double *cterm, const int *rflag, Shared &sh, int n,
+                                                          int lane, bool overlay, int k0, double phi, double phi_n) {
     const int ex_upto = sh.ex_upto;
     if (ex_upto < n) {
         const double C0 = ex_upto > 0 ? prefix[ex_upto - 1] : 0.0;
@@ -1259,9 +1263,9 @@ __device__ __attribute__((noinline)) double exact_sums(const double *term, doubl
     }
     if (k0 < n) {
         bool stopped = false;
-        *phi_n = wave_seq_sum(term + k0, n - k0, k0 > 0 ? prefix[k0 - 1] : 0.0, cprefix + k0, lane, nullptr, &stopped);
+        phi_n = wave_seq_sum(term + k0, n - k0, k0 > 0 ? prefix[k0 - 1] : 0.0, cprefix + k0, lane, nullptr, &stopped);
     }
-    return phi;
+    return ExactPhis{phi, phi_n};
 }
 
 // A scripted step's answer in the pinned output (wave 0; system-scope stores): [phi, k, (ray, ptS) x k],
@@ -2359,7 +2363,10 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
                             }
                         }
                         if (exact && k0 < n) {  // the committed partial sums and phi_r, then the proposal's
-                            phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, true, k0, phi_r, &phi_n);
+                            const ExactPhis ex = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane,
+                                                            true, k0, phi_r, phi_n);
+                            phi_r = ex.phi;
+                            phi_n = ex.phi_n;
                             if (prof_on && lane == 0) sh.prof[65] += 1;  // (diagnostic: exact decisions)
                         }
                         if (prof_on && lane == 0 && k0 < n) sh.prof[64] += n - k0;
@@ -2664,8 +2671,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
             if (prof_on && lane == 0) sh.prof[7 + action] += clock64() - sh.t_iter;  // per-action totals
             if ((rbx || xch) && it + 1 == round_end) {  // a tempering round is done: publish phi, take the next temperature
                 {  // (a phase F of this iteration made every sum exact already)
-                    double unused = 0.0;
-                    phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, false, n, phi_r, &unused);
+                    phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, false, n, phi_r, 0.0).phi;
                     if (lane == 0) sh.phi = phi_r;
                 }
                 if (rbx) {
@@ -2742,8 +2748,7 @@ __global__ __launch_bounds__(NTH, 2) void k_chain_run(const DevChain *__restrict
     const long long t_loop_end = prof_on ? clock64() : 0;
     {  // decisions on bounds: the partial sums and phi exact again (the launch leaves them)
         if (wv == 0) {
-            double unused = 0.0;
-            phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, false, n, phi_r, &unused);
+            phi_r = exact_sums(v.term, v.prefix, v.cprefix, v.cterm, v.rflag, sh, n, lane, false, n, phi_r, 0.0).phi;
             if (lane == 0) sh.phi = phi_r;
         }
         __syncthreads();

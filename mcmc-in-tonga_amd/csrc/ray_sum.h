@@ -23,7 +23,7 @@ __device__ __forceinline__ double seg_term_z(const double *__restrict__ w, const
 }
 
 template <class Z>
-__device__ __attribute__((noinline)) double julia_block_lane(const double *__restrict__ w, const Z &zeta, int s0, int f, int l) {
+__device__ __attribute__((noinline)) double julia_block_lane(const double *__restrict__ w, const Z zeta, int s0, int f, int l) {
     if (f == l) return seg_term_z(w, zeta, s0 + f);
     double v = seg_term_z(w, zeta, s0 + f) + seg_term_z(w, zeta, s0 + f + 1);
     const int T = l - f - 1;
@@ -49,7 +49,7 @@ __device__ __attribute__((noinline)) double julia_block_lane(const double *__res
 }
 
 template <class Z>
-__device__ __attribute__((noinline)) double julia_pairwise_lane(const double *__restrict__ w, const Z &zeta, int s0, int L) {
+__device__ __attribute__((noinline)) double julia_pairwise_lane(const double *__restrict__ w, const Z zeta, int s0, int L) {
     int ff[48], ll[48], st[48];
     double vals[48];
     int top = 1, nv = 0;
